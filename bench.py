@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""bench.py -- device-resident Bloom-filter build throughput (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c1]
+
+One step = one pass of the hot path over one batch: clear the filter words and
+build the filter from every key of the batch (hash + index + bit scatter), keys
+already resident in HBM.  N > 1 (torchrun, one rank per GPU): every rank builds
+its own independent filter over its own keys (the compaction fan-out, C4) --
+weak scaling, no data-path collective.  `value` = all keys of all ranks / the
+max-over-ranks time of the K timed steps.
+
+Extra fields: `roofline` (dominant kernel, HIP-event timed on its own stream;
+achieved = algorithmic bytes / average launch time) and, on rank 0 at
+N = 1, `cpu_baseline` (the reference BloomFilter.cpp compiled here, timed on a
+bounded sample of the same workload, 1 core).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "nasp-key-value-engine_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def algorithmic_bytes(n, key_len, total_key_bytes, m, var_len):
+    """keys read once, offsets read once, the filter written once."""
+    return total_key_bytes + (8 * (n + 1) if var_len else 0) + (m + 7) // 8
+
+
+def cpu_baseline(wl, keys_np, offs_np, key_len, budget_s=12.0):
+    """The reference add() loop (oracle/_ref: BloomFilter.cpp compiled here) on a
+    bounded prefix sample of this workload, 1 thread.  Falls back to the oracle
+    restatement (kind "port") if the reference build is absent."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    try:
+        from oracle_ctypes import RefLib
+        ref = RefLib()
+        kind = "reference"
+    except (FileNotFoundError, OSError):
+        ref = None
+        kind = "port"
+    from nasp_bloom.synth import H2_SEED
+    # calibrate on 100k keys, then size the sample to ~budget_s
+    n_cal = min(100_000, wl.n)
+
+    def run(nk):
+        if ref is not None:
+            return ref.build_timed(keys_np, offs_np, key_len, nk, wl.m, wl.k, H2_SEED)[0]
+        from oracle_ctypes import Oracle
+        t0 = time.perf_counter()
+        Oracle().build(0, keys_np, offs_np, key_len, nk, wl.m, wl.k, H2_SEED)
+        return time.perf_counter() - t0
+
+    t_cal = run(n_cal)
+    n_s = int(min(wl.n, max(n_cal, n_cal * budget_s / max(t_cal, 1e-9))))
+    t = run(n_s)
+    try:
+        cpu_model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
+    except Exception:  # noqa: BLE001
+        cpu_model = "unknown"
+    return {"value": round(n_s / t / 1e6, 4), "unit": "Mkeys/s", "cores": 1, "kind": kind,
+            "sample": f"first {n_s} keys of {wl.name} into the same m={wl.m}, k={wl.k} filter; "
+                      f"reference add() loop, {t:.1f} s, 1 thread ({cpu_model})"}
+
+
+def latest_traffic(workload_name):
+    """Per-launch HBM bytes of the build kernel from the committed PMC summary
+    (profiles/*pmc*.json, written by tools/pmc_traffic.py), or None."""
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:  # noqa: BLE001
+            continue
+        if d.get("workload") == workload_name and d.get("kernel_source_sha") == kernel_sha():
+            best = d
+    return best
+
+
+def kernel_sha():
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("csrc/bloom_kernels.hip", "csrc/bloom_math.h"):
+        h.update(open(os.path.join(REPO, "nasp-key-value-engine_amd", f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4"])
+    ap.add_argument("--flavor", type=int, default=0, help="0 libstdc++ (default), 1 MSVC FNV-1a")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    nbm.lib()  # fail loudly if the HIP library is missing
+
+    wl = synth.WORKLOADS[args.workload]
+    # each rank: its own independent key set (distinct generator seed) and filter
+    keys_np, offs_np, key_len = synth.keys_for(wl, seed=synth.SEED + rank)
+    var_len = offs_np is not None
+    total_key_bytes = int(offs_np[-1]) if var_len else wl.n * key_len
+    keys = torch.from_numpy(keys_np).to(dev)
+    offs = torch.from_numpy(offs_np.view(np.int64)).to(dev) if var_len else None
+    words = torch.zeros(nbm.nwords(wl.m), dtype=torch.int64, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+    seed = synth.H2_SEED
+
+    def step(ev=None):
+        with torch.cuda.stream(stream):
+            words.zero_()
+            if ev is not None:
+                ev[0].record(stream)
+            nbm.build_device(keys, offs, key_len, wl.n, wl.m, wl.k, seed, args.flavor, words,
+                             stream=stream)
+            if ev is not None:
+                ev[1].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    # correctness guard (cheap): every key of the batch must probe positive
+    probe_out = torch.empty(wl.n, dtype=torch.uint8, device=dev)
+    nbm.probe_device(keys, offs, key_len, wl.n, wl.m, wl.k, seed, args.flavor, words, probe_out)
+    torch.cuda.synchronize(dev)
+    if int(probe_out.min()) != 1:
+        raise SystemExit("build produced a false negative -- refusing to report")
+    del probe_out
+
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(events[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    total_keys = wl.n * args.steps * world
+    value = total_keys / elapsed / 1e6
+    B = algorithmic_bytes(wl.n, key_len, total_key_bytes, wl.m, var_len)
+    achieved = B / (kern_ms * 1e-3) / 1e9
+    pmc = latest_traffic(wl.name)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5),
+                "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
+                "kernel": "bloom_build_kernel", "kernel_ms": round(kern_ms, 5),
+                "algorithmic_bytes_per_launch": B,
+                "traffic_source": (pmc or {}).get("source")}
+
+    out = {"metric": "bloom-filter build Mkeys/s (device-resident, k=7), 1/2/4/8 GPU",
+           "value": round(value, 3), "unit": "Mkeys/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+           "data": "synthetic (splitmix64 keys, seed 0x5EED+rank)",
+           "config": {"workload": wl.name, "keys_per_gpu": wl.n,
+                      "key_bytes": key_len if key_len else f"{wl.lo}-{wl.hi} (var)",
+                      "m": wl.m, "k": wl.k, "h2_seed": seed,
+                      "flavor": ["libstdc++", "msvc-fnv1a"][args.flavor],
+                      "parallelism": f"independent filter per GPU x{world}"},
+           "roofline": roofline}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(wl, keys_np, offs_np, key_len, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

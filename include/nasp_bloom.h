@@ -1,0 +1,123 @@
+/*
+ * nasp_bloom.h -- C ABI of the MI355X-native SSTable Bloom-filter build/probe path.
+ *
+ * This is the drop-in boundary.  The reference has no FFI of its
+ * own: its callers use the C++ class `BloomFilter` (reference
+ * BloomFilter/BloomFilter.h:12-42) directly.  The replacement class in
+ * nasp-key-value-engine_amd/host/BloomFilter.h keeps that surface and calls the
+ * entry points below; any other language binds them the way INTEGRATION.md shows.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; nothing here throws.  Every function returns
+ *     NB_OK (0) or a negative NB_ERR_* code; nb_last_error() describes the last
+ *     failure of the calling thread.
+ *   - Keys are arbitrary bytes (embedded NUL and empty keys allowed), packed:
+ *       offsets != NULL : key i = keys[offsets[i] .. offsets[i+1]),  offsets has n+1 entries
+ *       offsets == NULL : key i = keys[i*key_len .. (i+1)*key_len)   (fixed-length keys)
+ *   - The filter is `words`: ceil(m/64) little-endian uint64 words; bit j of the
+ *     reference bitSet (BloomFilter.h:17) is bit (j % 64) of words[j / 64].  This
+ *     is byte-for-byte the bit payload of BloomFilter::serialize()
+ *     (BloomFilter.cpp:117-126).  Builds OR into `words` (never clear it), which
+ *     is the reference's add-after-deserialize semantics (TypesManager.cpp:84-86).
+ *   - The caller owns every buffer.  The library owns only cached device scratch
+ *     (per device) and releases it in nb_shutdown().
+ *   - Re-entrant per (device, stream).  Host-buffer entry points serialize on a
+ *     per-device lock around their cached scratch.
+ *   - Index function (BloomFilter.cpp:57-62):  idx_i = (h1 + i*h2) mod m in 64-bit
+ *     wrapping arithmetic, h1 = H(key), h2 = H(to_string(h2_seed) + key), where H is
+ *     std::hash<std::string> of the selected flavor.
+ */
+#ifndef NASP_BLOOM_H
+#define NASP_BLOOM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NB_ABI_VERSION 1
+
+enum nb_status {
+    NB_OK = 0,
+    NB_ERR_ARG = -1,      /* invalid argument (e.g. m == 0 with keys, k == 0, NULL buffer) */
+    NB_ERR_HIP = -2,      /* HIP runtime error (allocation, copy, launch) */
+    NB_ERR_NODEV = -3,    /* no usable gfx950 device */
+    NB_ERR_UNSUPPORTED = -4
+};
+
+/* Which std::hash<std::string> the reference binary was built with. */
+enum nb_flavor {
+    NB_FLAVOR_LIBSTDCXX = 0,  /* GCC libstdc++ std::_Hash_bytes(p, len, 0xc70f6907) (Linux build) */
+    NB_FLAVOR_MSVC_FNV1A = 1  /* MSVC STL FNV-1a-64 (the authors' Windows build) */
+};
+
+/* ---------------------------------------------------------------- info --- */
+int nb_abi_version(void);
+/* Number of visible HIP devices (0 when none). */
+int nb_device_count(void);
+/* Last error message of the calling thread ("" if none). */
+const char *nb_last_error(void);
+/* Release cached device scratch and streams on every device. */
+int nb_shutdown(void);
+
+/* ------------------------------------------------- parameter formulas --- */
+/* BloomFilter::calculateSizeOfBitSet (BloomFilter.cpp:192-194), including the
+ * reference's wrap modulo 2^32 of an out-of-range double->unsigned conversion. */
+uint32_t nb_size_of_bitset(uint32_t n, double p);
+/* BloomFilter::calculateNumberOfHashFunctions (BloomFilter.cpp:196-199). */
+uint32_t nb_num_hashes(uint32_t n, uint32_t m);
+/* h2_seed from timeConst: mt19937(timeConst) + uniform_int_distribution<uint64_t>
+ * (BloomFilter.cpp:37,44-46). */
+uint64_t nb_seed_from_time(uint32_t time_const);
+
+/* --------------------------------------------- host-buffer entry points --- */
+/* Replaces the add() loop of SSTable::build (SSTable/SSTable.cpp:31-34) and
+ * BloomFilter::add (BloomFilter.cpp:82-86) for a whole batch: uploads the keys,
+ * builds on `device`, ORs the result into the host `words`. */
+int nb_build(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+             uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
+             uint64_t *words, int device);
+
+/* Batch form of BloomFilter::possiblyContains (BloomFilter.cpp:67-80):
+ * out[i] = 1 if all k bits of key i are set, else 0.  k == 0 answers 1
+ * (the default-constructed filter, BloomFilter.cpp:26). */
+int nb_probe(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+             uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
+             const uint64_t *words, uint8_t *out, int device);
+
+/* ------------------------------------------ device-resident entry points --- */
+/* Same contracts; every pointer is device memory on the current device and
+ * the work is enqueued on `stream` (a hipStream_t; NULL = the null stream).
+ * No host synchronisation; graph-capturable. */
+int nb_build_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
+                    uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
+                    uint64_t *d_words, void *stream);
+
+int nb_probe_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
+                    uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
+                    const uint64_t *d_words, uint8_t *d_out, void *stream);
+
+/* d_dst[w] |= d_src[s*src_stride + w] for s < nsrc, w < nwords: the local OR step
+ * of the cooperative multi-GPU build (RCCL has no bitwise-OR reduction). */
+int nb_or_merge_device(uint64_t *d_dst, const uint64_t *d_src, uint64_t nwords,
+                       uint32_t nsrc, uint64_t src_stride, void *stream);
+
+/* ------------------------------------------------------ serialization --- */
+/* Size of BloomFilter::serialize()'s image: 28 + (uint32_t)(m+7)/8 bytes
+ * (BloomFilter.cpp:89-90; the (m+7) wraps in 32 bits exactly as the reference). */
+size_t nb_serialized_size(uint32_t m);
+/* BloomFilter::serialize (BloomFilter.cpp:88-129). Returns bytes written. */
+size_t nb_serialize(uint32_t m, uint32_t k, double p, uint32_t time_const, uint64_t h2_seed,
+                    const uint64_t *words, uint8_t *out);
+/* BloomFilter::deserialize (BloomFilter.cpp:131-190): header fields, and the bit
+ * payload into `words` (ceil(m/64) words; may be NULL to read the header only).
+ * Unlike the reference it checks `len` and returns NB_ERR_ARG if it is short. */
+int nb_deserialize(const uint8_t *img, size_t len, uint32_t *m, uint32_t *k, double *p,
+                   uint32_t *time_const, uint64_t *h2_seed, uint64_t *words);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NASP_BLOOM_H */

@@ -1,0 +1,61 @@
+// bloom_host.cpp -- host-only parts of the C ABI (include/nasp_bloom.h):
+// seed derivation and the serialized image.  No device code.
+//
+//   nb_seed_from_time  <- BloomFilter.cpp:37,44-46 (mt19937 + uniform_int_distribution)
+//   nb_serialize       <- BloomFilter.cpp:88-129
+//   nb_deserialize     <- BloomFilter.cpp:131-190
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <random>
+
+#include "../../include/nasp_bloom.h"
+
+extern "C" {
+
+uint64_t nb_seed_from_time(uint32_t time_const) {
+    std::mt19937 rng(time_const);
+    std::uniform_int_distribution<uint64_t> dist(0, std::numeric_limits<uint64_t>::max());
+    return dist(rng);
+}
+
+size_t nb_serialized_size(uint32_t m) {
+    // The reference computes (m + 7) / 8 in unsigned int: it wraps for m > 2^32-8.
+    return 28 + (size_t)((uint32_t)(m + 7u) / 8u);
+}
+
+size_t nb_serialize(uint32_t m, uint32_t k, double p, uint32_t time_const, uint64_t h2_seed,
+                    const uint64_t *words, uint8_t *out) {
+    std::memcpy(out + 0, &m, 4);
+    std::memcpy(out + 4, &k, 4);
+    std::memcpy(out + 8, &p, 8);
+    std::memcpy(out + 16, &time_const, 4);
+    std::memcpy(out + 20, &h2_seed, 8);
+    const size_t nbytes = (uint32_t)(m + 7u) / 8u;
+    // Little-endian u64 words are the LSB-first byte image (bit j -> byte j/8, bit j%8).
+    if (nbytes) std::memcpy(out + 28, words, nbytes);
+    return 28 + nbytes;
+}
+
+int nb_deserialize(const uint8_t *img, size_t len, uint32_t *m, uint32_t *k, double *p,
+                   uint32_t *time_const, uint64_t *h2_seed, uint64_t *words) {
+    if (!img || len < 28) return NB_ERR_ARG;
+    uint32_t mm;
+    std::memcpy(&mm, img + 0, 4);
+    if (m) *m = mm;
+    if (k) std::memcpy(k, img + 4, 4);
+    if (p) std::memcpy(p, img + 8, 8);
+    if (time_const) std::memcpy(time_const, img + 16, 4);
+    if (h2_seed) std::memcpy(h2_seed, img + 20, 8);
+    if (!words) return NB_OK;
+    const size_t nbytes = (uint32_t)(mm + 7u) / 8u;
+    if (len < 28 + nbytes) return NB_ERR_ARG;
+    const size_t nwords = ((size_t)mm + 63) / 64;
+    if (nwords) words[nwords - 1] = 0;  // clear the partial last word before the copy
+    if (nbytes) std::memcpy(words, img + 28, nbytes);
+    // Bits at positions >= m are ignored by the reference (BloomFilter.cpp:183).
+    if (mm & 63) words[nwords - 1] &= (1ull << (mm & 63)) - 1;
+    return NB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,287 @@
+// bloom_math.h -- index arithmetic of the reference filter, shared by the gfx950
+// kernels (bloom_kernels.hip) and the host-side parameter setup / single-key
+// probe of the drop-in class.  Header-only; NB_HD marks functions that are
+// compiled for both sides when the including TU is built by hipcc.
+//
+// What it computes (reference BloomFilter/BloomFilter.cpp:57-62):
+//   idx_i = (h1 + i*h2) mod m,   64-bit wrapping add/mul, m < 2^32
+//   h1 = H(key), h2 = H(to_string(h2_seed) + key)
+// with H = std::hash<std::string> of the selected flavour:
+//   libstdc++ _Hash_bytes(p, len, 0xc70f6907)  (MurmurHash2-64A-style, 8-byte words)
+//   MSVC FNV-1a-64                              (byte at a time)
+//
+// Two exact rewrites make this cheap on a GPU (both are proven equal to the
+// closure's arithmetic, and the parity tests check them bit for bit):
+//   1. mod by a runtime 32-bit m without a divide: normalized-reciprocal
+//      2-by-1 remainder (Moller & Granlund, "Improved division by invariant
+//      integers", 2011, Alg. 4) applied twice to the 96-bit shifted value.
+//   2. incremental indices: x_{i+1} = x_i + h2 (mod 2^64), so
+//      r_{i+1} = r_i + (h2 mod m) - [x_{i+1} wrapped] * (2^64 mod m)   (mod m),
+//      i.e. 2 true reductions per key instead of k.
+//   3. h2's seed prefix: the whole 8-byte words of to_string(seed) are mixed
+//      into constants once per filter (pre_d[]); the leftover r = D%8 prefix
+//      bytes are spliced in front of the key words with funnel shifts.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define NB_HD __host__ __device__ __forceinline__
+#else
+#define NB_HD inline
+#endif
+
+namespace nb {
+
+constexpr uint64_t kMul = 0xc6a4a7935bd1e995ULL;   // libstdc++ _Hash_bytes multiplier
+constexpr uint64_t kStdSeed = 0xc70f6907ULL;       // seed std::hash<string> passes
+constexpr uint64_t kFnvBasis = 14695981039346656037ULL;
+constexpr uint64_t kFnvPrime = 1099511628211ULL;   // 2^40 + 0x1b3
+
+NB_HD uint64_t shift_mix(uint64_t v) { return v ^ (v >> 47); }
+
+// One 8-byte word of the libstdc++ main loop.
+NB_HD uint64_t lsx_round(uint64_t h, uint64_t w) {
+    uint64_t d = shift_mix(w * kMul) * kMul;
+    return (h ^ d) * kMul;
+}
+// The (len & 7) tail: bytes loaded little-endian, no pre-mix.
+NB_HD uint64_t lsx_tail(uint64_t h, uint64_t t) { return (h ^ t) * kMul; }
+NB_HD uint64_t lsx_final(uint64_t h) { return shift_mix(shift_mix(h) * kMul); }
+NB_HD uint64_t lsx_init(uint64_t len) { return kStdSeed ^ (len * kMul); }
+
+NB_HD uint64_t fnv_step(uint64_t h, uint32_t byte) { return (h ^ byte) * kFnvPrime; }
+
+// ------------------------------------------------------------- fast mod ----
+struct FastMod {
+    uint32_t m;   // divisor (>= 1)
+    uint32_t l;   // clz32(m)
+    uint32_t d;   // m << l (top bit set)
+    uint32_t v;   // floor((2^64-1)/d) - 2^32
+};
+
+inline FastMod make_fastmod(uint32_t m) {
+    FastMod f;
+    f.m = m;
+    uint32_t l = 0;
+    while (l < 31 && !((m << l) & 0x80000000u)) ++l;
+    f.l = l;
+    f.d = m << l;
+    f.v = (uint32_t)(~0ULL / f.d - (1ULL << 32));
+    return f;
+}
+
+// Remainder of (u1:u0) / d, requires u1 < d, d normalized.
+NB_HD uint32_t rem_2by1(uint32_t u1, uint32_t u0, uint32_t d, uint32_t v) {
+    uint64_t q = (uint64_t)v * u1 + ((((uint64_t)u1 + 1) << 32) | u0);
+    uint32_t q1 = (uint32_t)(q >> 32), q0 = (uint32_t)q;
+    uint32_t r = u0 - q1 * d;
+    if (r > q0) r += d;
+    if (r >= d) r -= d;
+    return r;
+}
+
+NB_HD uint32_t mod64(uint64_t x, const FastMod &f) {
+    uint32_t n2 = f.l ? (uint32_t)(x >> (64 - f.l)) : 0u;
+    uint64_t xs = x << f.l;
+    uint32_t r = rem_2by1(n2, (uint32_t)(xs >> 32), f.d, f.v);
+    r = rem_2by1(r, (uint32_t)xs, f.d, f.v);
+    return r >> f.l;
+}
+
+// (a + b) mod m for a, b < m without 32-bit overflow.
+NB_HD uint32_t addmod(uint32_t a, uint32_t b, uint32_t m) {
+    return a >= m - b ? a - (m - b) : a + b;
+}
+NB_HD uint32_t submod(uint32_t a, uint32_t b, uint32_t m) {
+    return a >= b ? a - b : a + (m - b);
+}
+
+// ------------------------------------------------- per-filter constants ----
+constexpr int kMaxPrefixWords = 2;  // to_string(uint64) has <= 20 digits
+
+struct FilterConsts {
+    FastMod fm;
+    uint32_t k;
+    uint32_t c64;          // 2^64 mod m
+    uint32_t plen;         // D = number of decimal digits of h2_seed
+    uint32_t pwords;       // D / 8 whole prefix words
+    uint32_t prem;         // r = D % 8 leftover prefix bytes
+    uint32_t flavor;
+    uint64_t pre_d[kMaxPrefixWords];  // libstdc++: pre-mixed whole prefix words
+    uint64_t pre_tail;     // the r leftover prefix bytes, little-endian
+    uint64_t fnv_pre;      // FNV-1a state after all D prefix bytes
+};
+
+inline FilterConsts make_consts(uint32_t m, uint32_t k, uint64_t seed, uint32_t flavor) {
+    FilterConsts c{};
+    c.fm = make_fastmod(m);
+    c.k = k;
+    c.c64 = (uint32_t)((~0ULL % m + 1) % m);
+    char dig[24];
+    int n = 0;
+    {
+        char tmp[24];
+        uint64_t s = seed;
+        do { tmp[n++] = (char)('0' + s % 10); s /= 10; } while (s);
+        for (int i = 0; i < n; ++i) dig[i] = tmp[n - 1 - i];
+    }
+    c.plen = (uint32_t)n;
+    c.pwords = (uint32_t)n / 8;
+    c.prem = (uint32_t)n % 8;
+    c.flavor = flavor;
+    for (uint32_t w = 0; w < c.pwords; ++w) {
+        uint64_t x = 0;
+        for (int b = 0; b < 8; ++b) x |= (uint64_t)(uint8_t)dig[8 * w + b] << (8 * b);
+        c.pre_d[w] = shift_mix(x * kMul) * kMul;
+    }
+    uint64_t t = 0;
+    for (uint32_t b = 0; b < c.prem; ++b) t |= (uint64_t)(uint8_t)dig[8 * c.pwords + b] << (8 * b);
+    c.pre_tail = t;
+    uint64_t h = kFnvBasis;
+    for (int i = 0; i < n; ++i) h = fnv_step(h, (uint8_t)dig[i]);
+    c.fnv_pre = h;
+    return c;
+}
+
+
+// ------------------------------------------------- word-stream hashing ----
+// Both hashes of one key computed from its bytes viewed as 8-byte little-endian
+// words K_j (zero beyond len).  h2 hashes to_string(seed) ++ key: its whole
+// prefix words are pre-mixed (pre_d), and stream word j is the r = D%8 leftover
+// prefix bytes spliced in front of the key: S_j = K_{j-1} >> (64-8r) | K_j << 8r.
+
+NB_HD uint64_t mask_bytes(uint64_t w, int nbytes) {
+    return nbytes >= 8 ? w : (nbytes <= 0 ? 0ull : (w & ((1ull << (8 * nbytes)) - 1)));
+}
+
+// Bytes [a, a+8) of the 16-byte pair lo:hi; a8 = 8*a, a in [0, 8).
+NB_HD uint64_t funnel(uint64_t lo, uint64_t hi, uint32_t a8) {
+    return a8 ? (lo >> a8) | (hi << (64 - a8)) : lo;
+}
+
+struct LsxState {
+    uint64_t h1, h2, kprev;
+};
+
+NB_HD void lsx_begin(const FilterConsts &c, LsxState &s, uint32_t len) {
+    s.h1 = lsx_init(len);
+    uint64_t g = lsx_init((uint64_t)len + c.plen);
+    for (int w = 0; w < kMaxPrefixWords; ++w)
+        if ((uint32_t)w < c.pwords) g = (g ^ c.pre_d[w]) * kMul;
+    s.h2 = g;
+    s.kprev = c.prem ? c.pre_tail << (64 - 8 * c.prem) : 0;
+}
+
+// Feed key word j (zero beyond len) into both hashes.
+NB_HD void lsx_consume(const FilterConsts &c, LsxState &s, uint32_t j, uint64_t kw,
+                       uint32_t len) {
+    if (j < (len >> 3)) s.h1 = lsx_round(s.h1, kw);
+    else s.h1 = lsx_tail(s.h1, kw);  // only reached when len & 7 != 0
+    const uint32_t r8 = 8 * c.prem;
+    const uint64_t sw = r8 ? (s.kprev >> (64 - r8)) | (kw << r8) : kw;
+    s.kprev = kw;
+    const uint32_t slen = len + c.prem;
+    if (j < (slen >> 3)) s.h2 = lsx_round(s.h2, sw);
+    else if (slen & 7) s.h2 = lsx_tail(s.h2, sw);
+}
+
+NB_HD void lsx_end(const FilterConsts &c, LsxState &s, uint32_t len, uint64_t *h1,
+                   uint64_t *h2) {
+    const uint32_t nk = (len + 7) >> 3;
+    const uint32_t slen = len + c.prem;
+    if (((slen + 7) >> 3) > nk) {  // one more stream word: the last key word's high bytes
+        const uint64_t sw = s.kprev >> (64 - 8 * c.prem);
+        if (nk < (slen >> 3)) s.h2 = lsx_round(s.h2, sw);
+        else s.h2 = lsx_tail(s.h2, sw);
+    }
+    *h1 = lsx_final(s.h1);
+    *h2 = lsx_final(s.h2);
+}
+
+NB_HD void fnv_consume(uint64_t &h1, uint64_t &h2, uint64_t kw, int nbytes) {
+    for (int b = 0; b < 8; ++b) {
+        if (b < nbytes) {
+            const uint32_t byte = (uint32_t)(kw >> (8 * b)) & 0xffu;
+            h1 = fnv_step(h1, byte);
+            h2 = fnv_step(h2, byte);
+        }
+    }
+}
+
+// Hash a key whose first byte sits at byte a (0..7) of aligned word Q(0);
+// Q(j) returns aligned word j.  Only words holding at least one key byte are read.
+template <int FLAVOR, class LoadQ>
+NB_HD void hash_aligned_words(const FilterConsts &c, LoadQ Q, uint32_t a, uint32_t len,
+                              uint64_t *h1, uint64_t *h2) {
+    const uint32_t nq = (a + len + 7) >> 3;
+    const uint32_t nk = (len + 7) >> 3;
+    uint64_t qcur = nq ? Q(0) : 0;
+    if (FLAVOR == 1) {
+        uint64_t f1 = kFnvBasis, f2 = c.fnv_pre;
+        for (uint32_t j = 0; j < nk; ++j) {
+            const uint64_t qnext = (j + 1 < nq) ? Q(j + 1) : 0;
+            const uint64_t kw = funnel(qcur, qnext, 8 * a);
+            qcur = qnext;
+            fnv_consume(f1, f2, kw, (int)(len - 8 * j));
+        }
+        *h1 = f1;
+        *h2 = f2;
+    } else {
+        LsxState s;
+        lsx_begin(c, s, len);
+        for (uint32_t j = 0; j < nk; ++j) {
+            const uint64_t qnext = (j + 1 < nq) ? Q(j + 1) : 0;
+            const uint64_t kw = mask_bytes(funnel(qcur, qnext, 8 * a), (int)(len - 8 * j));
+            qcur = qnext;
+            lsx_consume(c, s, j, kw, len);
+        }
+        lsx_end(c, s, len, h1, h2);
+    }
+}
+
+// -------------------------------------------------------- host reference ----
+// Scalar host evaluation over a contiguous key (used for the single-key probe of
+// the drop-in class; the batch paths run on the device).
+inline void key_hashes_host(const FilterConsts &c, const uint8_t *p, uint64_t len,
+                            uint64_t *h1o, uint64_t *h2o) {
+    auto ld = [](const uint8_t *q, uint64_t nb) {
+        uint64_t r = 0;
+        for (uint64_t b = 0; b < nb; ++b) r |= (uint64_t)q[b] << (8 * b);
+        return r;
+    };
+    if (c.flavor == 1) {
+        uint64_t a = kFnvBasis, b = c.fnv_pre;
+        for (uint64_t i = 0; i < len; ++i) { a = fnv_step(a, p[i]); b = fnv_step(b, p[i]); }
+        *h1o = a; *h2o = b;
+        return;
+    }
+    uint64_t h = lsx_init(len);
+    uint64_t whole = len & ~7ULL;
+    for (uint64_t o = 0; o < whole; o += 8) h = lsx_round(h, ld(p + o, 8));
+    if (len & 7) h = lsx_tail(h, ld(p + whole, len & 7));
+    *h1o = lsx_final(h);
+    // h2 over prefix ++ key, with the whole prefix words pre-mixed.
+    uint64_t total = c.plen + len;
+    uint64_t g = lsx_init(total);
+    for (uint32_t w = 0; w < c.pwords; ++w) g = (g ^ c.pre_d[w]) * kMul;
+    // stream = r prefix bytes ++ key bytes
+    uint64_t slen = c.prem + len;
+    uint64_t swhole = slen & ~7ULL;
+    auto sbyte = [&](uint64_t i) -> uint64_t {
+        return i < c.prem ? (c.pre_tail >> (8 * i)) & 0xff : p[i - c.prem];
+    };
+    for (uint64_t o = 0; o < swhole; o += 8) {
+        uint64_t w = 0;
+        for (int b = 0; b < 8; ++b) w |= sbyte(o + b) << (8 * b);
+        g = lsx_round(g, w);
+    }
+    if (slen & 7) {
+        uint64_t w = 0;
+        for (uint64_t b = 0; b < (slen & 7); ++b) w |= sbyte(swhole + b) << (8 * b);
+        g = lsx_tail(g, w);
+    }
+    *h2o = lsx_final(g);
+}
+
+}  // namespace nb

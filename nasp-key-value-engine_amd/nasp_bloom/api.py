@@ -1,0 +1,215 @@
+"""Python surface over the C ABI.
+
+Device entry points take torch tensors that already live on the GPU (the
+device-resident hot path); host entry points take numpy arrays.  The
+`BloomFilter` class mirrors the reference class (BloomFilter/BloomFilter.h:24-41)
+with the same names, argument meaning and semantics:
+  - default-constructed filter: possiblyContains() is True (BloomFilter.cpp:26,67-80)
+  - add() after deserialize() ORs into the existing bits (TypesManager.cpp:84-86)
+  - serialize() is byte-identical to the reference image (BloomFilter.cpp:88-129)
+Adds are batched inside the object and built on the GPU when the filter is read.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import time
+
+import numpy as np
+
+from ._lib import FLAVOR_LIBSTDCXX, NaspBloomError, check, lib
+
+
+def nwords(m: int) -> int:
+    """u64 words holding m bits (the device/host filter layout)."""
+    return (int(m) + 63) // 64
+
+
+def size_of_bitset(n: int, p: float) -> int:
+    return int(lib().nb_size_of_bitset(n, p))
+
+
+def num_hashes(n: int, m: int) -> int:
+    return int(lib().nb_num_hashes(n, m))
+
+
+def seed_from_time(time_const: int) -> int:
+    return int(lib().nb_seed_from_time(time_const))
+
+
+def _stream_handle(stream) -> int | None:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return getattr(stream, "cuda_stream", stream)
+
+
+def _check_device_args(keys, offsets, words):
+    if not keys.is_cuda or not words.is_cuda:
+        raise NaspBloomError("device entry points need CUDA (HIP) tensors")
+    if offsets is not None and not offsets.is_cuda:
+        raise NaspBloomError("offsets must be on the device")
+    if not words.is_contiguous() or not keys.is_contiguous():
+        raise NaspBloomError("keys and words must be contiguous")
+
+
+def build_device(keys, offsets, key_len: int, n: int, m: int, k: int, seed: int, flavor: int,
+                 words, stream=None) -> None:
+    """OR the k bits of n device-resident keys into `words` (int64/uint64 cuda tensor)."""
+    _check_device_args(keys, offsets, words)
+    if words.numel() * words.element_size() < nwords(m) * 8:
+        raise NaspBloomError("words tensor smaller than ceil(m/64) u64 words")
+    rc = lib().nb_build_device(keys.data_ptr(), offsets.data_ptr() if offsets is not None else None,
+                               key_len, n, m, k, seed, flavor, words.data_ptr(),
+                               _stream_handle(stream))
+    check(rc, "nb_build_device")
+
+
+def probe_device(keys, offsets, key_len: int, n: int, m: int, k: int, seed: int, flavor: int,
+                 words, out, stream=None) -> None:
+    """out[i] (uint8 cuda tensor) = 1 if all k bits of key i are set."""
+    _check_device_args(keys, offsets, words)
+    rc = lib().nb_probe_device(keys.data_ptr(), offsets.data_ptr() if offsets is not None else None,
+                               key_len, n, m, k, seed, flavor, words.data_ptr(), out.data_ptr(),
+                               _stream_handle(stream))
+    check(rc, "nb_probe_device")
+
+
+def or_merge_device(dst, src, nwords_: int, nsrc: int, src_stride: int, stream=None) -> None:
+    rc = lib().nb_or_merge_device(dst.data_ptr(), src.data_ptr(), nwords_, nsrc, src_stride,
+                                  _stream_handle(stream))
+    check(rc, "nb_or_merge_device")
+
+
+def _np_ptr(a):
+    return None if a is None else a.ctypes.data
+
+
+def build_host(keys: np.ndarray, offsets: np.ndarray | None, key_len: int, n: int, m: int, k: int,
+               seed: int, flavor: int, words: np.ndarray, device: int = 0) -> None:
+    """Host buffers in, host words OR-accumulated out (H2D + kernel + D2H)."""
+    assert words.dtype == np.uint64 and words.flags.c_contiguous
+    rc = lib().nb_build(_np_ptr(keys), _np_ptr(offsets), key_len, n, m, k, seed, flavor,
+                        _np_ptr(words), device)
+    check(rc, "nb_build")
+
+
+def probe_host(keys: np.ndarray, offsets: np.ndarray | None, key_len: int, n: int, m: int, k: int,
+               seed: int, flavor: int, words: np.ndarray, device: int = 0) -> np.ndarray:
+    out = np.zeros(max(n, 1), dtype=np.uint8)
+    rc = lib().nb_probe(_np_ptr(keys), _np_ptr(offsets), key_len, n, m, k, seed, flavor,
+                        _np_ptr(words), _np_ptr(out), device)
+    check(rc, "nb_probe")
+    return out[:n]
+
+
+def serialize(m: int, k: int, p: float, time_const: int, seed: int, words: np.ndarray) -> bytes:
+    size = lib().nb_serialized_size(m)
+    out = np.zeros(size, dtype=np.uint8)
+    w = words if words.size else np.zeros(1, np.uint64)
+    n = lib().nb_serialize(m, k, p, time_const, seed, _np_ptr(w), _np_ptr(out))
+    return out[:n].tobytes()
+
+
+def deserialize(img: bytes):
+    """-> (m, k, p, time_const, seed, words)"""
+    buf = np.frombuffer(img, dtype=np.uint8).copy()
+    m, k, tc, seed = C.c_uint32(), C.c_uint32(), C.c_uint32(), C.c_uint64()
+    p = C.c_double()
+    rc = lib().nb_deserialize(_np_ptr(buf), len(img), C.addressof(m), C.addressof(k),
+                              C.addressof(p), C.addressof(tc), C.addressof(seed), None)
+    check(rc, "nb_deserialize(header)")
+    words = np.zeros(max(nwords(m.value), 1), dtype=np.uint64)
+    rc = lib().nb_deserialize(_np_ptr(buf), len(img), None, None, None, None, None, _np_ptr(words))
+    check(rc, "nb_deserialize")
+    return m.value, k.value, p.value, tc.value, seed.value, words
+
+
+def _pack(keys: list[bytes]):
+    offs = np.zeros(len(keys) + 1, dtype=np.uint64)
+    if keys:
+        offs[1:] = np.cumsum([len(x) for x in keys], dtype=np.uint64)
+    flat = b"".join(keys)
+    buf = np.frombuffer(flat + b"\0" * 16, dtype=np.uint8).copy()
+    return buf, offs
+
+
+class BloomFilter:
+    """Mirror of the reference `BloomFilter` (BloomFilter/BloomFilter.h:12-42)."""
+
+    BATCH_LIMIT = 1 << 20  # pending keys before an automatic device build
+
+    def __init__(self, n: int | None = None, falsePositiveRate: float | None = None, *,
+                 flavor: int = FLAVOR_LIBSTDCXX, device: int = 0, time_const: int | None = None):
+        self.flavor = flavor
+        self.device = device
+        self._pending: list[bytes] = []
+        if n is None:  # BloomFilter() -- BloomFilter.cpp:26: no closures, no bits
+            self.m, self.k, self.p, self.timeConst, self.h2_seed = 0, 0, 0.0, 0, 0
+            self.words = np.zeros(1, dtype=np.uint64)
+            return
+        self.m = self.calculateSizeOfBitSet(n, falsePositiveRate)
+        self.k = self.calculateNumberOfHashFunctions(n, self.m)
+        self.p = float(falsePositiveRate)
+        self.timeConst = (int(time.time()) if time_const is None else int(time_const)) & 0xFFFFFFFF
+        self.h2_seed = seed_from_time(self.timeConst)
+        self.words = np.zeros(max(nwords(self.m), 1), dtype=np.uint64)
+
+    # -- reference static helpers (BloomFilter.cpp:192-199)
+    @staticmethod
+    def calculateSizeOfBitSet(expectedElements: int, falsePositiveRate: float) -> int:
+        return size_of_bitset(expectedElements, falsePositiveRate)
+
+    @staticmethod
+    def calculateNumberOfHashFunctions(expectedElements: int, m: int) -> int:
+        return num_hashes(expectedElements, m)
+
+    # -- batching
+    def _flush(self) -> None:
+        if not self._pending:
+            return
+        keys, self._pending = self._pending, []
+        if self.k == 0:
+            return  # no closures: add() sets nothing (BloomFilter.cpp:82-86)
+        buf, offs = _pack(keys)
+        build_host(buf, offs, 0, len(keys), self.m, self.k, self.h2_seed, self.flavor,
+                   self.words, self.device)
+
+    def add(self, elem: bytes | str) -> None:
+        self._pending.append(elem.encode() if isinstance(elem, str) else bytes(elem))
+        if len(self._pending) >= self.BATCH_LIMIT:
+            self._flush()
+
+    def add_batch(self, elems) -> None:
+        for e in elems:
+            self._pending.append(e.encode() if isinstance(e, str) else bytes(e))
+        if len(self._pending) >= self.BATCH_LIMIT:
+            self._flush()
+
+    def possiblyContains(self, elem: bytes | str) -> bool:
+        return bool(self.possiblyContainsBatch([elem])[0])
+
+    def possiblyContainsBatch(self, elems) -> np.ndarray:
+        self._flush()
+        keys = [e.encode() if isinstance(e, str) else bytes(e) for e in elems]
+        if self.k == 0:
+            return np.ones(len(keys), dtype=np.uint8)
+        buf, offs = _pack(keys)
+        return probe_host(buf, offs, 0, len(keys), self.m, self.k, self.h2_seed, self.flavor,
+                          self.words, self.device)
+
+    def serialize(self) -> bytes:
+        self._flush()
+        return serialize(self.m, self.k, self.p, self.timeConst, self.h2_seed, self.words)
+
+    @staticmethod
+    def deserialize(data: bytes, *, flavor: int = FLAVOR_LIBSTDCXX, device: int = 0) -> "BloomFilter":
+        bf = BloomFilter(flavor=flavor, device=device)
+        bf.m, bf.k, bf.p, bf.timeConst, bf.h2_seed, bf.words = deserialize(data)
+        return bf
+
+    def copy(self) -> "BloomFilter":
+        self._flush()
+        bf = BloomFilter(flavor=self.flavor, device=self.device)
+        bf.m, bf.k, bf.p, bf.timeConst, bf.h2_seed = self.m, self.k, self.p, self.timeConst, self.h2_seed
+        bf.words = self.words.copy()
+        return bf

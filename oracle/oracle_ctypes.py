@@ -141,6 +141,9 @@ class RefLib:
                                   C.c_double, C.c_uint32, C.c_uint64, _u8p, _u8p]
         lib.ref_probe.restype = C.c_int
         lib.ref_probe.argtypes = [_u8p, C.c_uint64, _u8p, _u64p, C.c_uint32, C.c_uint64, _u8p]
+        lib.ref_build_timed.restype = C.c_double
+        lib.ref_build_timed.argtypes = [_u8p, _u64p, C.c_uint32, C.c_uint64, C.c_uint32,
+                                        C.c_uint32, C.c_uint64, _u8p, C.c_uint64]
         lib.ref_default_contains.restype = C.c_int
         lib.ref_default_contains.argtypes = [_u8p, C.c_uint64]
         self.lib = lib
@@ -169,6 +172,14 @@ class RefLib:
         self.lib.ref_build(_ptr(keys_u8), _ptr(offsets, _u64p), key_len, n, m, k, p, tc, seed,
                            _ptr(init), _ptr(out))
         return out.tobytes()
+
+    def build_timed(self, keys_u8, offsets, key_len, n, m, k, seed) -> tuple[float, bytes]:
+        """Seconds spent in the reference add() loop, and the serialized image."""
+        size = 28 + ((m + 7) & 0xFFFFFFFF) // 8
+        out = np.zeros(size, dtype=np.uint8)
+        secs = self.lib.ref_build_timed(_ptr(keys_u8), _ptr(offsets, _u64p), key_len, n, m, k,
+                                        seed, _ptr(out), size)
+        return secs, out.tobytes()
 
     def probe(self, image: bytes, keys_u8, offsets, key_len, n):
         img = np.frombuffer(image, dtype=np.uint8).copy()

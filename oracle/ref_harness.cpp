@@ -10,6 +10,8 @@
 // (BloomFilter.cpp:131-190), then keys go through the reference add()
 // (BloomFilter.cpp:82-86) one std::string at a time, exactly as SSTable::build
 // does (SSTable/SSTable.cpp:28-35).
+#include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstring>
 #include <functional>
@@ -84,6 +86,27 @@ int ref_build(const uint8_t* keys, const uint64_t* offs, uint32_t key_len, uint6
     std::vector<std::byte> res = bf.serialize();
     std::memcpy(out, res.data(), res.size());
     return 0;
+}
+
+// Timed form for bench.py's cpu_baseline: the same add() loop, with only the
+// loop itself inside the clock (deserialize/serialize are O(m) setup).
+double ref_build_timed(const uint8_t* keys, const uint64_t* offs, uint32_t key_len, uint64_t n,
+                       uint32_t m, uint32_t k, uint64_t seed, uint8_t* out_first_bytes,
+                       uint64_t nout) {
+    std::vector<std::byte> img = header_only(m, k, 0.01, 0, seed);
+    BloomFilter bf = BloomFilter::deserialize(img);
+    std::string s;
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t i = 0; i < n; ++i) {
+        key_at(keys, offs, key_len, i, s);
+        bf.add(s);
+    }
+    auto t1 = std::chrono::steady_clock::now();
+    if (out_first_bytes && nout) {
+        std::vector<std::byte> res = bf.serialize();
+        std::memcpy(out_first_bytes, res.data(), std::min<uint64_t>(nout, res.size()));
+    }
+    return std::chrono::duration<double>(t1 - t0).count();
 }
 
 // Probe `n` keys against a serialized image.

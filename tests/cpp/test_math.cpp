@@ -1,0 +1,76 @@
+// Host check of bloom_math.h against plain 64-bit arithmetic and the oracle:
+// fast remainder, incremental indices, and both hash flavours (with the seed
+// prefix splice).  Built and run by tests/test_math_host.py (no GPU needed).
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+#include "../../nasp-key-value-engine_amd/csrc/bloom_math.h"
+extern "C" {
+#include "../../oracle/bloom_oracle.h"
+}
+
+int main() {
+    std::mt19937_64 rng(12345);
+    long bad = 0;
+    std::vector<uint32_t> ms = {1u, 2u, 3u, 7u, 20u, 64u, 47926u, 95850584u, 958505838u,
+                                1492685679u, 2147483648u, 2147483659u, 3000000019u,
+                                4294967288u, 4294967295u};
+    for (int t = 0; t < 2000; ++t) ms.push_back((uint32_t)(rng() >> (rng() % 32)) | 1u);
+    for (uint32_t m : ms) {
+        nb::FastMod f = nb::make_fastmod(m);
+        for (int t = 0; t < 2000; ++t) {
+            uint64_t x = rng();
+            if (t < 8) x = t < 4 ? (uint64_t)t : ~0ull - (uint64_t)(t - 4);
+            if (nb::mod64(x, f) != (uint32_t)(x % m)) ++bad;
+        }
+        // incremental indices vs direct
+        nb::FilterConsts c = nb::make_consts(m, 10, 17027509906831645879ull, 0);
+        for (int t = 0; t < 200; ++t) {
+            uint64_t h1 = rng(), h2 = rng();
+            uint32_t r = nb::mod64(h1, c.fm), s = nb::mod64(h2, c.fm);
+            uint64_t x = h1;
+            for (uint32_t i = 0; i < 40; ++i) {
+                if (i) {
+                    uint64_t nx = x + h2;
+                    r = nb::addmod(r, s, m);
+                    if (nx < x) r = nb::submod(r, c.c64, m);
+                    x = nx;
+                }
+                if (r != (uint32_t)((h1 + (uint64_t)i * h2) % m)) ++bad;
+            }
+        }
+    }
+    printf("mod/incremental mismatches: %ld\n", bad);
+    long hbad = 0;
+    uint64_t seeds[] = {0ull, 5ull, 12345678ull, 123456789ull, 1234567890123456ull,
+                        17027509906831645879ull, 18446744073709551615ull, 99999999ull};
+    for (uint64_t seed : seeds) {
+        for (int fl = 0; fl < 2; ++fl) {
+            nb::FilterConsts c = nb::make_consts(1000003u, 7, seed, (uint32_t)fl);
+            for (int t = 0; t < 3000; ++t) {
+                uint8_t buf[100];
+                size_t len = rng() % 90;
+                for (size_t b = 0; b < len; ++b) buf[b] = (uint8_t)rng();
+                uint64_t h1, h2;
+                nb::key_hashes_host(c, buf, len, &h1, &h2);
+                // the device's word-stream path, at every misalignment a = 0..7
+                alignas(8) uint8_t arena[128 + 16];
+                uint32_t a = (uint32_t)(rng() % 8);
+                for (size_t b = 0; b < sizeof arena; ++b) arena[b] = (uint8_t)rng();  // junk around
+                for (size_t b = 0; b < len; ++b) arena[8 + a + b] = buf[b];
+                const uint64_t *q = reinterpret_cast<const uint64_t *>(arena + 8);
+                uint64_t g1, g2;
+                if (fl) nb::hash_aligned_words<1>(c, [q](uint32_t j) { return q[j]; }, a, (uint32_t)len, &g1, &g2);
+                else nb::hash_aligned_words<0>(c, [q](uint32_t j) { return q[j]; }, a, (uint32_t)len, &g1, &g2);
+                if (g1 != h1 || g2 != h2) ++hbad;
+                for (uint32_t i = 0; i < 3; ++i) {
+                    uint32_t want = orc_index(fl, buf, len, i, 1000003u, seed);
+                    if ((uint32_t)((h1 + (uint64_t)i * h2) % 1000003u) != want) ++hbad;
+                }
+            }
+        }
+    }
+    printf("hash mismatches: %ld\n", hbad);
+    return (bad || hbad) ? 1 : 0;
+}

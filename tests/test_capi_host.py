@@ -1,0 +1,89 @@
+"""C ABI checks that need no GPU: the library loads, exports every symbol the
+header declares, and its host-only functions (formulas, seed, serialize,
+deserialize) agree with the golden vectors.  No compute entry point is called."""
+import os
+import re
+import struct
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+from golden_util import image_of, words_of_bits
+
+
+def header_symbols():
+    text = open(os.path.join(REPO, "include", "nasp_bloom.h")).read()
+    return sorted(set(re.findall(r"\b(nb_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_exports_every_header_symbol(built):
+    import nasp_bloom
+    from nasp_bloom import _lib
+    h = nasp_bloom.lib()
+    syms = header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(h, s), s
+        assert s in _lib._SIGS, f"{s} has no ctypes signature"
+    assert h.nb_abi_version() == 1
+
+
+def test_no_device_is_reported_not_faked(built):
+    import nasp_bloom
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    h = nasp_bloom.lib()
+    assert h.nb_device_count() == 0
+
+
+def test_formulas_and_seed(built, golden):
+    import nasp_bloom as nbm
+    lib, msvc = golden
+    for f in lib["formulas"]:
+        assert nbm.size_of_bitset(f["n"], f["p"]) == f["m"]
+        if f["k"] is not None:
+            assert nbm.num_hashes(f["n"], f["m"]) == f["k"]
+    for f in msvc["filters"]:
+        raw = bytes.fromhex(f["bytes_hex"])
+        tc, seed = struct.unpack("<IQ", raw[8 + 16:8 + 28])
+        assert nbm.seed_from_time(tc) == seed
+
+
+def test_serialize_roundtrip_golden(built, golden):
+    import nasp_bloom as nbm
+    lib, msvc = golden
+    for c in lib["build_cases"][:40]:
+        img = image_of(c)
+        m, k, p, tc, seed, words = nbm.deserialize(img)
+        assert (m, k) == (c["m"], c["k"])
+        assert nbm.serialize(m, k, p, tc, seed, words) == img
+        np.testing.assert_array_equal(words[:(m + 63) // 64], words_of_bits(m, c["bits"])[:(m + 63) // 64])
+    for f in msvc["filters"]:
+        img = bytes.fromhex(f["bytes_hex"])[8:]
+        assert nbm.serialize(*nbm.deserialize(img)) == img
+
+
+def test_deserialize_rejects_short_image(built):
+    import nasp_bloom as nbm
+    with pytest.raises(nbm.NaspBloomError):
+        nbm.deserialize(b"\x01" * 10)
+    hdr = struct.pack("<IIdIQ", 1000, 3, 0.01, 1, 5)
+    with pytest.raises(nbm.NaspBloomError):
+        nbm.deserialize(hdr + b"\0" * 10)  # needs 125 payload bytes
+
+
+def test_serialized_size_wraps_like_reference(built):
+    import nasp_bloom as nbm
+    h = nbm.lib()
+    assert h.nb_serialized_size(20) == 31
+    assert h.nb_serialized_size(2**32 - 8) == 28 + (2**32 - 1) // 8
+    assert h.nb_serialized_size(2**32 - 1) == 28  # (m+7) wraps in unsigned int
+
+
+def test_default_filter_contains_everything(built):
+    import nasp_bloom as nbm
+    bf = nbm.BloomFilter()
+    assert bf.possiblyContains(b"anything")  # no closures -> true (no device needed)
+    assert bf.serialize()[:8] == b"\0" * 8
