@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -85,26 +86,41 @@ __device__ __forceinline__ void hashes_of(const FilterConsts &c, const uint8_t *
 
 // ------------------------------------------------------------- kernels ----
 
+// Index stream of one key: r_0 = h1 mod m, then r_{j+1} = r_j + (h2 mod m) with a
+// -(2^64 mod m) correction whenever the 64-bit x_j = h1 + j*h2 wraps.
+struct IndexGen {
+    uint64_t x, h2;
+    uint32_t r, s;
+    __device__ __forceinline__ void start(uint64_t h1_, uint64_t h2_, const FilterConsts &c) {
+        x = h1_;
+        h2 = h2_;
+        r = nb::mod64(h1_, c.fm);
+        s = nb::mod64(h2_, c.fm);
+    }
+    __device__ __forceinline__ void next(const FilterConsts &c) {
+        const uint64_t nx = x + h2;
+        r = nb::addmod(r, s, c.fm.m);
+        if (nx < x) r = nb::submod(r, c.c64, c.fm.m);
+        x = nx;
+    }
+};
+
+// Path A ("atomic"): one lane per key, k no-return agent-scope atomic ORs.
+// Bounded by the chip's atomic request rate (~27 G/s measured, tools/ubench.hip),
+// used for k > 16, for filters too large for the tiled path, and for tiny batches.
 template <int FLAVOR, int LAYOUT>
-__global__ __launch_bounds__(kBlock) void bloom_build_kernel(
+__global__ __launch_bounds__(kBlock) void bloom_build_atomic_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
     uint64_t n, FilterConsts c, uint32_t *__restrict__ words32) {
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         uint64_t h1, h2;
         hashes_of<FLAVOR, LAYOUT>(c, keys, offsets, key_len, i, &h1, &h2);
-        const uint32_t m = c.fm.m;
-        uint32_t r = nb::mod64(h1, c.fm);
-        const uint32_t s2 = nb::mod64(h2, c.fm);
-        uint64_t x = h1;
+        IndexGen g;
+        g.start(h1, h2, c);
         for (uint32_t j = 0; j < c.k; ++j) {
-            if (j) {
-                const uint64_t nx = x + h2;
-                r = nb::addmod(r, s2, m);
-                if (nx < x) r = nb::submod(r, c.c64, m);
-                x = nx;
-            }
-            __hip_atomic_fetch_or(words32 + (r >> 5), 1u << (r & 31), __ATOMIC_RELAXED,
+            if (j) g.next(c);
+            __hip_atomic_fetch_or(words32 + (g.r >> 5), 1u << (g.r & 31), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
         }
     }
@@ -118,21 +134,180 @@ __global__ __launch_bounds__(kBlock) void bloom_probe_kernel(
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         uint64_t h1, h2;
         hashes_of<FLAVOR, LAYOUT>(c, keys, offsets, key_len, i, &h1, &h2);
-        const uint32_t m = c.fm.m;
-        uint32_t r = nb::mod64(h1, c.fm);
-        const uint32_t s2 = nb::mod64(h2, c.fm);
-        uint64_t x = h1;
+        IndexGen g;
+        g.start(h1, h2, c);
         uint8_t hit = 1;
         for (uint32_t j = 0; j < c.k; ++j) {
-            if (j) {
-                const uint64_t nx = x + h2;
-                r = nb::addmod(r, s2, m);
-                if (nx < x) r = nb::submod(r, c.c64, m);
-                x = nx;
-            }
-            if (!((words32[r >> 5] >> (r & 31)) & 1u)) { hit = 0; break; }
+            if (j) g.next(c);
+            if (!((words32[g.r >> 5] >> (g.r & 31)) & 1u)) { hit = 0; break; }
         }
         out[i] = hit;
+    }
+}
+
+
+// Path B ("tiled"): the filter is cut into T tiles of 2^ts bits.
+//   bin kernel : hash KPB keys per block, rank every index inside its tile with
+//                an LDS counter, counting-sort the block's indices in LDS, reserve
+//                a run per tile in that tile's global bucket (one contiguous-lane
+//                atomicAdd per tile per block), and write the runs out coalesced.
+//   tile kernel: one block per tile: OR the tile's bucket into a zeroed LDS copy
+//                (ds_or, ~1.4 T ops/s chip-wide), then OR the tile into the filter
+//                words with coalesced 8-byte loads/stores.
+// Buckets hold the full 32-bit index.  A bucket that would exceed its capacity
+// (only for pathological inputs, e.g. massively duplicated keys) spills the extra
+// indices straight into the filter with atomic ORs, so results never depend on it.
+struct TileCfg {
+    uint32_t ts;     // log2 bits per tile
+    uint32_t T;      // number of tiles = ceil(m / 2^ts)
+    uint32_t cap;    // bucket capacity (entries) per tile, multiple of 4
+};
+
+constexpr int kBinThreads = 512;
+constexpr int kTileThreads = 1024;
+
+// Exclusive scan of hist[0..T) into S[0..T); returns the total.  blockDim = kBinThreads.
+__device__ uint32_t block_exclusive_scan(const uint32_t *hist, uint32_t *S, uint32_t T,
+                                         uint32_t *wave_sums) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t per = (T + kBinThreads - 1) / kBinThreads;
+    const uint32_t b = min(tid * per, T), e = min(b + per, T);
+    uint32_t local = 0;
+    for (uint32_t t = b; t < e; ++t) local += hist[t];
+    uint32_t incl = local;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t v = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += v;
+    }
+    if (lane == 63) wave_sums[wid] = incl;
+    __syncthreads();
+    if (wid == 0) {
+        uint32_t w = lane < kBinThreads / 64 ? wave_sums[lane] : 0;
+        uint32_t wi = w;
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            uint32_t v = __shfl_up(wi, d, 64);
+            if (lane >= (uint32_t)d) wi += v;
+        }
+        if (lane < kBinThreads / 64) wave_sums[lane] = wi - w;  // exclusive wave offsets
+        if (lane == kBinThreads / 64 - 1) wave_sums[kBinThreads / 64] = wi;  // total
+    }
+    __syncthreads();
+    uint32_t run = wave_sums[wid] + incl - local;
+    for (uint32_t t = b; t < e; ++t) {
+        S[t] = run;
+        run += hist[t];
+    }
+    return wave_sums[kBinThreads / 64];
+}
+
+template <int FLAVOR, int LAYOUT, int KPT, int KMAX>
+__global__ __launch_bounds__(kBinThreads) void bloom_bin_kernel(
+    const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
+    uint64_t n, FilterConsts c, TileCfg tc, uint32_t *__restrict__ gcur,
+    uint32_t *__restrict__ buckets, uint32_t *__restrict__ words32) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t T = tc.T;
+    uint32_t *hist = lds;              // [T]
+    uint32_t *S = hist + T;            // [T] block-local run starts
+    uint32_t *G = S + T;               // [T] global run starts (bucket positions)
+    uint32_t *wave_sums = G + T;       // [kBinThreads/64 + 1]
+    uint32_t *sorted = wave_sums + 32; // [KPB * k]
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t t = tid; t < T; t += kBinThreads) hist[t] = 0;
+    __syncthreads();
+
+    // phase 1: hash, indices, in-tile ranks (kept in registers)
+    uint32_t idx[KPT][KMAX], rnk[KPT][KMAX];
+    const uint64_t base = (uint64_t)blockIdx.x * (KPT * kBinThreads);
+#pragma unroll
+    for (int p = 0; p < KPT; ++p) {
+        const uint64_t i = base + (uint64_t)p * kBinThreads + tid;
+        if (i < n) {
+            uint64_t h1, h2;
+            hashes_of<FLAVOR, LAYOUT>(c, keys, offsets, key_len, i, &h1, &h2);
+            IndexGen g;
+            g.start(h1, h2, c);
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j) {
+                if ((uint32_t)j < c.k) {
+                    if (j) g.next(c);
+                    idx[p][j] = g.r;
+                    rnk[p][j] = atomicAdd(&hist[g.r >> tc.ts], 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+
+    // phase 2: block-local run starts and global reservations
+    const uint32_t total = block_exclusive_scan(hist, S, T, wave_sums);
+    for (uint32_t t = tid; t < T; t += kBinThreads) {
+        const uint32_t h = hist[t];
+        G[t] = h ? atomicAdd(&gcur[t], h) : 0u;
+    }
+    __syncthreads();
+
+    // phase 3: counting-sort the block's indices by tile
+#pragma unroll
+    for (int p = 0; p < KPT; ++p) {
+        const uint64_t i = base + (uint64_t)p * kBinThreads + tid;
+        if (i < n) {
+#pragma unroll
+            for (int j = 0; j < KMAX; ++j)
+                if ((uint32_t)j < c.k) sorted[S[idx[p][j] >> tc.ts] + rnk[p][j]] = idx[p][j];
+        }
+    }
+    __syncthreads();
+
+    // phase 4: coalesced write-out of the runs (spill beyond capacity)
+    for (uint32_t j = tid; j < total; j += kBinThreads) {
+        const uint32_t v = sorted[j];
+        const uint32_t t = v >> tc.ts;
+        const uint32_t pos = G[t] + (j - S[t]);
+        if (pos < tc.cap)
+            buckets[(size_t)t * tc.cap + pos] = v;
+        else
+            __hip_atomic_fetch_or(words32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__global__ __launch_bounds__(kTileThreads) void bloom_tile_or_kernel(
+    TileCfg tc, uint32_t *__restrict__ gcur, const uint32_t *__restrict__ buckets,
+    uint64_t *__restrict__ words, uint64_t nwords) {
+    extern __shared__ uint32_t tile[];
+    const uint32_t t = blockIdx.x, tid = threadIdx.x;
+    const uint32_t tile_words32 = 1u << (tc.ts - 5);
+    const uint32_t mask = (1u << tc.ts) - 1;
+    for (uint32_t w = tid; w < tile_words32; w += kTileThreads) tile[w] = 0;
+    __syncthreads();
+    const uint32_t cnt = min(gcur[t], tc.cap);
+    const uint32_t *e = buckets + (size_t)t * tc.cap;
+    const uint4 *e4 = reinterpret_cast<const uint4 *>(e);
+    for (uint32_t q = tid; q < cnt / 4; q += kTileThreads) {
+        const uint4 v = e4[q];
+        atomicOr(&tile[(v.x & mask) >> 5], 1u << (v.x & 31));
+        atomicOr(&tile[(v.y & mask) >> 5], 1u << (v.y & 31));
+        atomicOr(&tile[(v.z & mask) >> 5], 1u << (v.z & 31));
+        atomicOr(&tile[(v.w & mask) >> 5], 1u << (v.w & 31));
+    }
+    for (uint32_t q = (cnt & ~3u) + tid; q < cnt; q += kTileThreads) {
+        const uint32_t v = e[q];
+        atomicOr(&tile[(v & mask) >> 5], 1u << (v & 31));
+    }
+    __syncthreads();
+    if (tid == 0) gcur[t] = 0;  // the workspace invariant: cursors are zero between builds
+    const uint64_t w0 = (uint64_t)t << (tc.ts - 6);
+    const uint32_t tile_words64 = tile_words32 / 2;
+    const uint64_t *tile64 = reinterpret_cast<const uint64_t *>(tile);
+    for (uint32_t w = tid; w < tile_words64; w += kTileThreads) {
+        const uint64_t gw = w0 + w;
+        if (gw < nwords) {
+            const uint64_t v = tile64[w];
+            if (v) words[gw] |= v;
+        }
     }
 }
 
@@ -178,22 +353,156 @@ int check_common(uint64_t n, uint32_t m, int flavor, const void *keys, const voi
     return NB_OK;
 }
 
+// Per-(device, stream) scratch of the tiled path: tile cursors (kept zero between
+// builds by the tile kernel) and the bucket array.
+struct Workspace {
+    int dev = -1;
+    hipStream_t st = nullptr;
+    uint32_t *gcur = nullptr;
+    size_t gcur_cap = 0;     // entries
+    uint32_t *buckets = nullptr;
+    size_t bucket_cap = 0;   // entries
+};
+std::mutex g_ws_mu;
+std::vector<Workspace *> g_ws;
+
+int get_ws(hipStream_t st, Workspace **out) {
+    int dev = 0;
+    NB_HIP(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    for (Workspace *w : g_ws)
+        if (w->dev == dev && w->st == st) { *out = w; return NB_OK; }
+    Workspace *w = new Workspace;
+    w->dev = dev;
+    w->st = st;
+    g_ws.push_back(w);
+    *out = w;
+    return NB_OK;
+}
+
+int ws_reserve(Workspace &w, uint32_t T, size_t entries) {
+    if (T > w.gcur_cap || entries > w.bucket_cap) NB_HIP(hipStreamSynchronize(w.st));
+    if (T > w.gcur_cap) {
+        if (w.gcur) NB_HIP(hipFree(w.gcur));
+        w.gcur = nullptr;
+        w.gcur_cap = 0;
+        const size_t want = std::max<size_t>(T, 4096);
+        NB_HIP(hipMalloc(&w.gcur, want * 4));
+        NB_HIP(hipMemset(w.gcur, 0, want * 4));
+        w.gcur_cap = want;
+    }
+    if (entries > w.bucket_cap) {
+        if (w.buckets) NB_HIP(hipFree(w.buckets));
+        w.buckets = nullptr;
+        w.bucket_cap = 0;
+        const size_t want = entries + entries / 8;
+        NB_HIP(hipMalloc(&w.buckets, want * 4));
+        w.bucket_cap = want;
+    }
+    return NB_OK;
+}
+
+TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
+    TileCfg tc;
+    uint32_t ts = 12;  // floor(log2(m / 256)) clamped to [12, 20]: >= 256 tiles when possible
+    while (ts < 20 && ((uint64_t)m >> (ts + 1)) >= 256) ++ts;
+    tc.ts = ts;
+    tc.T = (uint32_t)(((uint64_t)m + (1ull << ts) - 1) >> ts);
+    const double e = (double)n_chunk * k / tc.T;
+    uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
+    cap = (cap + 63) & ~63ull;
+    tc.cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFC0ull);
+    return tc;
+}
+
+enum class BuildPath { kAuto, kAtomic, kTiled };
+
+BuildPath path_override() {
+    const char *e = std::getenv("NB_BUILD_PATH");
+    if (!e) return BuildPath::kAuto;
+    if (!std::strcmp(e, "atomic")) return BuildPath::kAtomic;
+    if (!std::strcmp(e, "tiled")) return BuildPath::kTiled;
+    return BuildPath::kAuto;
+}
+
+uint64_t chunk_keys() {
+    const char *e = std::getenv("NB_CHUNK_KEYS");
+    uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
+    return v ? v : (1ull << 27);
+}
+
+template <class K>
+int allow_lds(K kernel, size_t bytes) {
+    if (bytes > 64 * 1024)
+        NB_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(kernel),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    return NB_OK;
+}
+
+template <int FLAVOR, int LAYOUT>
+int launch_atomic(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                  const FilterConsts &c, uint64_t *words, hipStream_t st) {
+    hipLaunchKernelGGL((bloom_build_atomic_kernel<FLAVOR, LAYOUT>), dim3(grid_for(n)),
+                       dim3(kBlock), 0, st, keys, offsets, key_len, n, c,
+                       reinterpret_cast<uint32_t *>(words));
+    NB_HIP(hipGetLastError());
+    return NB_OK;
+}
+
+template <int FLAVOR, int LAYOUT, int KPT, int KMAX>
+int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                 const FilterConsts &c, uint64_t *words, hipStream_t st) {
+    constexpr uint64_t kpb = (uint64_t)KPT * kBinThreads;
+    const uint64_t chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, chunk_keys()));
+    const TileCfg tc = choose_tiles(c.fm.m, chunk, c.k);
+    Workspace *ws;
+    int rc;
+    if ((rc = get_ws(st, &ws))) return rc;
+    if ((rc = ws_reserve(*ws, tc.T, (size_t)tc.T * tc.cap))) return rc;
+    const size_t bin_lds = (3ull * tc.T + 32 + kpb * c.k) * 4;
+    const size_t tile_lds = (size_t)1 << (tc.ts - 3);
+    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, KMAX>;
+    if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(bloom_tile_or_kernel, tile_lds))) return rc;
+    const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
+    uint32_t *w32 = reinterpret_cast<uint32_t *>(words);
+    for (uint64_t done = 0; done < n; done += chunk) {
+        const uint64_t cn = std::min(chunk, n - done);
+        const uint8_t *ck = offsets ? keys : keys + done * key_len;
+        const uint64_t *co = offsets ? offsets + done : nullptr;
+        hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(kBinThreads), bin_lds,
+                           st, ck, co, key_len, cn, c, tc, ws->gcur, ws->buckets, w32);
+        NB_HIP(hipGetLastError());
+        hipLaunchKernelGGL(bloom_tile_or_kernel, dim3(tc.T), dim3(kTileThreads), tile_lds, st, tc,
+                           ws->gcur, ws->buckets, words, nwords);
+        NB_HIP(hipGetLastError());
+    }
+    return NB_OK;
+}
+
+template <int FLAVOR, int LAYOUT>
+int launch_build_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                   const FilterConsts &c, uint64_t *words, hipStream_t st) {
+    BuildPath p = path_override();
+    if (p == BuildPath::kAuto) {
+        const TileCfg tc = choose_tiles(c.fm.m, n, c.k);
+        const bool ok = c.k <= 16 && tc.T <= 2048 && n >= 4096;
+        p = ok ? BuildPath::kTiled : BuildPath::kAtomic;
+    }
+    if (p == BuildPath::kTiled && c.k <= 16 && choose_tiles(c.fm.m, 1, c.k).T <= 2048) {
+        if (c.k <= 8) return launch_tiled<FLAVOR, LAYOUT, 4, 8>(keys, offsets, key_len, n, c, words, st);
+        return launch_tiled<FLAVOR, LAYOUT, 2, 16>(keys, offsets, key_len, n, c, words, st);
+    }
+    return launch_atomic<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, st);
+}
+
 template <int FLAVOR>
 int launch_build_f(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                    const FilterConsts &c, uint64_t *words, hipStream_t st) {
-    dim3 grid(grid_for(n)), block(kBlock);
-    uint32_t *w32 = reinterpret_cast<uint32_t *>(words);
     if (!offsets && key_len == 16 && (reinterpret_cast<uintptr_t>(keys) & 15) == 0)
-        hipLaunchKernelGGL((bloom_build_kernel<FLAVOR, kFixed16>), grid, block, 0, st, keys,
-                           offsets, key_len, n, c, w32);
-    else if (!offsets)
-        hipLaunchKernelGGL((bloom_build_kernel<FLAVOR, kFixedStride>), grid, block, 0, st, keys,
-                           offsets, key_len, n, c, w32);
-    else
-        hipLaunchKernelGGL((bloom_build_kernel<FLAVOR, kOffsets>), grid, block, 0, st, keys,
-                           offsets, key_len, n, c, w32);
-    NB_HIP(hipGetLastError());
-    return NB_OK;
+        return launch_build_l<FLAVOR, kFixed16>(keys, offsets, key_len, n, c, words, st);
+    if (!offsets)
+        return launch_build_l<FLAVOR, kFixedStride>(keys, offsets, key_len, n, c, words, st);
+    return launch_build_l<FLAVOR, kOffsets>(keys, offsets, key_len, n, c, words, st);
 }
 
 template <int FLAVOR>
@@ -300,6 +609,17 @@ int nb_device_count(void) {
 const char *nb_last_error(void) { return g_last_error.c_str(); }
 
 int nb_shutdown(void) {
+    {
+        std::lock_guard<std::mutex> lk(g_ws_mu);
+        for (Workspace *w : g_ws) {
+            (void)hipSetDevice(w->dev);
+            (void)hipStreamSynchronize(w->st);
+            if (w->gcur) (void)hipFree(w->gcur);
+            if (w->buckets) (void)hipFree(w->buckets);
+            delete w;
+        }
+        g_ws.clear();
+    }
     for (int i = 0; i < kMaxDev; ++i) {
         DevScratch &d = g_dev[i];
         std::lock_guard<std::mutex> lk(d.mu);

@@ -28,6 +28,13 @@ def dev(built):
     return torch.device("cuda:0")
 
 
+@pytest.fixture(params=["auto", "atomic", "tiled"])
+def build_path(request, monkeypatch):
+    """Run a test through each build path of the library (NB_BUILD_PATH)."""
+    monkeypatch.setenv("NB_BUILD_PATH", request.param)
+    return request.param
+
+
 def t_u8(a, dev):
     import torch
     return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
@@ -70,7 +77,7 @@ def dev_probe(dev, buf, offs, key_len, n, m, k, seed, words, flavor=0):
 
 # ---------------------------------------------------------------- golden --
 
-def test_golden_build_cases(dev, golden):
+def test_golden_build_cases(dev, golden, build_path):
     import nasp_bloom as nbm
     lib, _ = golden
     for c in lib["build_cases"]:
@@ -82,7 +89,7 @@ def test_golden_build_cases(dev, golden):
         assert img == image_of(c), (c["keys"], c["m"], c["k"])
 
 
-def test_golden_msvc_filters_device(dev, golden):
+def test_golden_msvc_filters_device(dev, golden, build_path):
     import nasp_bloom as nbm
     _, msvc = golden
     for f in msvc["filters"]:
@@ -107,7 +114,7 @@ def test_golden_probe_cases(dev, golden):
         assert dev_probe(dev, buf, offs, 0, len(q), m, k, seed, words).tolist() == c["answer"]
 
 
-def test_golden_accumulate(dev, golden):
+def test_golden_accumulate(dev, golden, build_path):
     """add() after deserialize() ORs into the existing bits (TypesManager.cpp:84-86)."""
     lib, _ = golden
     keys = keys_of(lib, "var8_64")
@@ -119,7 +126,7 @@ def test_golden_accumulate(dev, golden):
         np.testing.assert_array_equal(w, words_of_bits(m, c["final"]["bits"]))
 
 
-def test_golden_large_m(dev, golden):
+def test_golden_large_m(dev, golden, build_path):
     lib, _ = golden
     for c in lib["large_m"]:
         key = bytes.fromhex(c["key_hex"])
@@ -132,7 +139,7 @@ def test_golden_large_m(dev, golden):
 # ------------------------------------------------------ configs vs oracle --
 
 @pytest.mark.parametrize("cfg", ["c1", "c2"])
-def test_fixed16_configs_full_size(dev, oracle, cfg):
+def test_fixed16_configs_full_size(dev, oracle, cfg, build_path):
     from nasp_bloom import synth
     w = synth.WORKLOADS[cfg]
     buf, offs, kl = synth.keys_for(w)
@@ -143,7 +150,7 @@ def test_fixed16_configs_full_size(dev, oracle, cfg):
 
 @pytest.mark.parametrize("flavor", [0, 1])
 @pytest.mark.parametrize("shift", [0, 3])
-def test_varlen_c3_shape(dev, oracle, flavor, shift):
+def test_varlen_c3_shape(dev, oracle, flavor, shift, build_path):
     from nasp_bloom import synth
     n = 2_000_000 if flavor == 0 else 500_000
     buf, offs = synth.var_keys(n)
@@ -153,7 +160,7 @@ def test_varlen_c3_shape(dev, oracle, flavor, shift):
 
 
 @pytest.mark.parametrize("key_len,shift", [(16, 4), (32, 0), (7, 1), (1, 0), (64, 5), (100, 0)])
-def test_fixed_stride_layouts(dev, oracle, key_len, shift):
+def test_fixed_stride_layouts(dev, oracle, key_len, shift, build_path):
     from nasp_bloom import synth
     n = 200_003
     buf = synth.fixed_keys(n, key_len, seed=key_len)
@@ -165,7 +172,7 @@ def test_fixed_stride_layouts(dev, oracle, key_len, shift):
 
 
 @pytest.mark.parametrize("seed", [0, 7, 12345678, 123456789, 1234567890123456789, 2**64 - 1])
-def test_seed_prefix_lengths(dev, oracle, seed):
+def test_seed_prefix_lengths(dev, oracle, seed, build_path):
     """to_string(seed) of 1..20 digits changes how the prefix splices into h2."""
     from nasp_bloom import synth
     buf, offs = synth.var_keys(100_000, 0, 40)
@@ -187,7 +194,7 @@ def test_c5_shape_sample(dev, oracle):
 
 
 @pytest.mark.parametrize("m", [1, 2, 63, 64, 65, 2**31, 2**32 - 8, 2**32 - 1])
-def test_edge_m(dev, oracle, m):
+def test_edge_m(dev, oracle, m, build_path):
     from nasp_bloom import synth
     buf, offs = synth.var_keys(20_000, 0, 24)
     for k in (1, 10):
@@ -196,7 +203,7 @@ def test_edge_m(dev, oracle, m):
         np.testing.assert_array_equal(got, want)
 
 
-def test_empty_and_degenerate(dev, oracle):
+def test_empty_and_degenerate(dev, oracle, build_path):
     import nasp_bloom as nbm
     import torch
     # n = 0: no-op
@@ -216,6 +223,44 @@ def test_empty_and_degenerate(dev, oracle):
     w0 = dev_build(dev, np.zeros(48, np.uint8), None, 16, 3, 1000, 0, SEED)
     assert not w0.any()
     assert dev_probe(dev, np.zeros(48, np.uint8), None, 16, 3, 1000, 0, SEED, w0).tolist() == [1, 1, 1]
+
+
+@pytest.mark.parametrize("k", [1, 8, 9, 16, 17, 24])
+def test_k_range_tiled(dev, oracle, k, monkeypatch):
+    """k selects the tiled kernel's register layout (<=8, <=16) or the atomic path (>16)."""
+    from nasp_bloom import synth
+    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    buf, offs = synth.var_keys(300_000, 4, 40)
+    got = dev_build(dev, buf, offs, 0, 300_000, 7_000_003, k, SEED)
+    want = oracle.build(0, buf, offs, 0, 300_000, 7_000_003, k, SEED)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_tiled_bucket_overflow_spill(dev, oracle, monkeypatch):
+    """Massively duplicated keys overflow the per-tile buckets; the spill path must
+    still give the exact filter (SSTable keys are unique, but the API allows this)."""
+    from nasp_bloom import synth
+    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    n = 400_000
+    buf = np.zeros(n * 16 + 16, np.uint8)  # 400k identical all-zero 16-byte keys
+    buf[: 16 * 1000] = synth.fixed_keys(1000, 16)[: 16 * 1000]  # + 1000 distinct ones
+    got = dev_build(dev, buf, None, 16, n, 95_850_584, 7, SEED)
+    want = oracle.build(0, buf, None, 16, n, 95_850_584, 7, SEED)
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("chunk", ["4096", "100000", "999999"])
+def test_tiled_chunking(dev, oracle, chunk, monkeypatch):
+    from nasp_bloom import synth
+    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    monkeypatch.setenv("NB_CHUNK_KEYS", chunk)
+    buf, offs = synth.var_keys(1_000_000)
+    got = dev_build(dev, buf, offs, 0, 1_000_000, 9_585_059, 7, SEED)
+    want = oracle.build(0, buf, offs, 0, 1_000_000, 9_585_059, 7, SEED)
+    np.testing.assert_array_equal(got, want)
+    fixed = synth.fixed_keys(700_001, 16)
+    got = dev_build(dev, fixed, None, 16, 700_001, 95_850_584, 7, SEED)
+    np.testing.assert_array_equal(got, oracle.build(0, fixed, None, 16, 700_001, 95_850_584, 7, SEED))
 
 
 def test_probe_parity(dev, oracle):
