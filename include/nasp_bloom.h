@@ -90,10 +90,23 @@ int nb_probe(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uin
 /* ------------------------------------------ device-resident entry points --- */
 /* Same contracts; every pointer is device memory on the current device and
  * the work is enqueued on `stream` (a hipStream_t; NULL = the null stream).
- * No host synchronisation; graph-capturable. */
+ * No host synchronisation once the library's per-(device, stream) workspace is
+ * large enough; the first call with a larger shape grows it (hipMalloc, stream
+ * synchronised), so warm a stream up with its largest shape before capturing it
+ * into a hipGraph. */
 int nb_build_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
                     uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
                     uint64_t *d_words, void *stream);
+
+/* Flags of nb_build_device_ex. */
+#define NB_BUILD_OVERWRITE 1u /* d_words := filter of this batch (a fresh filter, as
+                                 SSTable::build makes; SSTable/SSTable.cpp:28) instead
+                                 of OR-accumulating into it */
+
+/* nb_build_device with flags (0 = exactly nb_build_device). */
+int nb_build_device_ex(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
+                       uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
+                       uint64_t *d_words, uint32_t flags, void *stream);
 
 int nb_probe_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
                     uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,

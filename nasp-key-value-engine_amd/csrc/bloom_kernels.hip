@@ -41,13 +41,14 @@ constexpr int kBlock = 256;
 // bloom_math.h so the host test (tests/cpp/test_math.cpp) runs the same code.
 using nb::LsxState;
 
-template <int FLAVOR>
+template <int FLAVOR, bool FIXED_LEN>
 __device__ __forceinline__ void key_hashes_ptr(const FilterConsts &c, const uint8_t *p,
                                                uint32_t len, uint64_t *h1, uint64_t *h2) {
     const uintptr_t addr = reinterpret_cast<uintptr_t>(p);
     const uint32_t a = (uint32_t)(addr & 7);
     const uint64_t *q = reinterpret_cast<const uint64_t *>(addr - a);
-    nb::hash_aligned_words<FLAVOR>(c, [q](uint32_t j) { return q[j]; }, a, len, h1, h2);
+    auto load = [q](uint32_t j) { return q[j]; };
+    nb::hash_aligned_words<FLAVOR, decltype(load), FIXED_LEN>(c, load, a, len, h1, h2);
 }
 
 // Fixed 16-byte keys, 16-byte aligned: one dwordx4 load per lane.
@@ -63,7 +64,7 @@ __device__ __forceinline__ void key_hashes_16(const FilterConsts &c, const uint8
         *h2 = f2;
     } else {
         LsxState s;
-        nb::lsx_begin(c, s, 16);
+        nb::lsx_begin_fixed(c, s, 16);
         nb::lsx_consume(c, s, 0, kv.x, 16);
         nb::lsx_consume(c, s, 1, kv.y, 16);
         nb::lsx_end(c, s, 16, h1, h2);
@@ -77,10 +78,10 @@ __device__ __forceinline__ void hashes_of(const FilterConsts &c, const uint8_t *
     if (LAYOUT == kFixed16) {
         key_hashes_16<FLAVOR>(c, keys, i, h1, h2);
     } else if (LAYOUT == kFixedStride) {
-        key_hashes_ptr<FLAVOR>(c, keys + i * key_len, key_len, h1, h2);
+        key_hashes_ptr<FLAVOR, true>(c, keys + i * key_len, key_len, h1, h2);
     } else {
         uint64_t b = offsets[i], e = offsets[i + 1];
-        key_hashes_ptr<FLAVOR>(c, keys + b, (uint32_t)(e - b), h1, h2);
+        key_hashes_ptr<FLAVOR, false>(c, keys + b, (uint32_t)(e - b), h1, h2);
     }
 }
 
@@ -147,30 +148,46 @@ __global__ __launch_bounds__(kBlock) void bloom_probe_kernel(
 
 
 // Path B ("tiled"): the filter is cut into T tiles of 2^ts bits.
-//   bin kernel : hash KPB keys per block, rank every index inside its tile with
-//                an LDS counter, counting-sort the block's indices in LDS, reserve
-//                a run per tile in that tile's global bucket (one contiguous-lane
-//                atomicAdd per tile per block), and write the runs out coalesced.
-//   tile kernel: one block per tile: OR the tile's bucket into a zeroed LDS copy
-//                (ds_or, ~1.4 T ops/s chip-wide), then OR the tile into the filter
-//                words with coalesced 8-byte loads/stores.
-// Buckets hold the full 32-bit index.  A bucket that would exceed its capacity
-// (only for pathological inputs, e.g. massively duplicated keys) spills the extra
-// indices straight into the filter with atomic ORs, so results never depend on it.
+//   bin kernel : hash KPB keys per block, count every index per tile in LDS,
+//                reserve one run per tile in that tile's bucket (contiguous-lane
+//                atomicAdds on cursors sharded G ways by block -- blocks b and b+8
+//                share an XCD, so a shard's runs are written through one L2),
+//                counting-sort the block's indices in LDS and write the runs out.
+//   tile kernel: one block per tile: OR the tile's G bucket shards into a zeroed
+//                LDS copy (ds_or), then store the tile into the filter words
+//                (overwrite) or OR it in (accumulate).
+// Bucket entries are the in-tile bit offset: 16-bit when ts <= 16 (half the
+// traffic), else the full 32-bit index.  A shard that would exceed its capacity
+// (pathological inputs only, e.g. massively duplicated keys) spills the extra
+// indices into a zero-kept spill bitmap that the tile kernel folds in and clears,
+// so results never depend on capacity.
 struct TileCfg {
     uint32_t ts;     // log2 bits per tile
     uint32_t T;      // number of tiles = ceil(m / 2^ts)
-    uint32_t cap;    // bucket capacity (entries) per tile, multiple of 4
+    uint32_t G;      // cursor/bucket shards per tile
+    uint32_t cap;    // capacity (entries) of one (tile, shard) bucket, multiple of 8
 };
 
-constexpr int kBinThreads = 512;
+constexpr int kBinThreads = 1024;
+constexpr int kBinKPT = 2;       // keys per thread when k <= 8 (1 for larger k)
 constexpr int kTileThreads = 1024;
+constexpr int kTileUnroll = 2;   // 16-byte bucket loads in flight per lane
+constexpr int kShards = 8;
+constexpr uint32_t kMaxTiles = 4096;
 
-// Exclusive scan of hist[0..T) into S[0..T); returns the total.  blockDim = kBinThreads.
+// Diagnostic builds (tools/ubench_tiled.hip) stop a kernel after a phase to price
+// it; in the product this is compiled out.
+#ifndef NB_DIAG_STOP
+#define NB_DIAG_STOP(phase) false
+#endif
+
+// Exclusive scan of hist[0..T) into S[0..T); returns the total.  blockDim = NT.
+template <int NT>
 __device__ uint32_t block_exclusive_scan(const uint32_t *hist, uint32_t *S, uint32_t T,
                                          uint32_t *wave_sums) {
+    constexpr uint32_t kWaves = NT / 64;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t per = (T + kBinThreads - 1) / kBinThreads;
+    const uint32_t per = (T + NT - 1) / NT;
     const uint32_t b = min(tid * per, T), e = min(b + per, T);
     uint32_t local = 0;
     for (uint32_t t = b; t < e; ++t) local += hist[t];
@@ -183,15 +200,15 @@ __device__ uint32_t block_exclusive_scan(const uint32_t *hist, uint32_t *S, uint
     if (lane == 63) wave_sums[wid] = incl;
     __syncthreads();
     if (wid == 0) {
-        uint32_t w = lane < kBinThreads / 64 ? wave_sums[lane] : 0;
+        uint32_t w = lane < kWaves ? wave_sums[lane] : 0;
         uint32_t wi = w;
 #pragma unroll
-        for (int d = 1; d < 16; d <<= 1) {
+        for (int d = 1; d < (int)kWaves; d <<= 1) {
             uint32_t v = __shfl_up(wi, d, 64);
             if (lane >= (uint32_t)d) wi += v;
         }
-        if (lane < kBinThreads / 64) wave_sums[lane] = wi - w;  // exclusive wave offsets
-        if (lane == kBinThreads / 64 - 1) wave_sums[kBinThreads / 64] = wi;  // total
+        if (lane < kWaves) wave_sums[lane] = wi - w;  // exclusive wave offsets
+        if (lane == kWaves - 1) wave_sums[kWaves] = wi;  // total
     }
     __syncthreads();
     uint32_t run = wave_sums[wid] + incl - local;
@@ -199,114 +216,182 @@ __device__ uint32_t block_exclusive_scan(const uint32_t *hist, uint32_t *S, uint
         S[t] = run;
         run += hist[t];
     }
-    return wave_sums[kBinThreads / 64];
+    return wave_sums[kWaves];
 }
 
-template <int FLAVOR, int LAYOUT, int KPT, int KMAX>
-__global__ __launch_bounds__(kBinThreads) void bloom_bin_kernel(
+struct TileScratch {
+    uint32_t *gcur;       // [G][T] bucket cursors (zero between builds)
+    uint32_t *spill_flag; // [T]    (zero between builds)
+    uint32_t *spill32;    // [2*ceil(m/64)] spill bitmap (zero between builds)
+};
+
+template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY, int NT = kBinThreads>
+__global__ __launch_bounds__(NT) void bloom_bin_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
-    uint64_t n, FilterConsts c, TileCfg tc, uint32_t *__restrict__ gcur,
-    uint32_t *__restrict__ buckets, uint32_t *__restrict__ words32) {
+    uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc, ENTRY *__restrict__ buckets) {
     extern __shared__ uint32_t lds[];
     const uint32_t T = tc.T;
-    uint32_t *hist = lds;              // [T]
-    uint32_t *S = hist + T;            // [T] block-local run starts
-    uint32_t *G = S + T;               // [T] global run starts (bucket positions)
-    uint32_t *wave_sums = G + T;       // [kBinThreads/64 + 1]
+    uint32_t *cnt = lds;               // [T] per-tile counts, then placement cursors
+    uint32_t *S = cnt + T;             // [T] block-local run starts
+    uint32_t *G = S + T;               // [T] bucket positions of the runs
+    uint32_t *wave_sums = G + T;       // [NT/64 + 1]
     uint32_t *sorted = wave_sums + 32; // [KPB * k]
     const uint32_t tid = threadIdx.x;
-    for (uint32_t t = tid; t < T; t += kBinThreads) hist[t] = 0;
+    for (uint32_t t = tid; t < T; t += NT) cnt[t] = 0;
     __syncthreads();
 
-    // phase 1: hash, indices, in-tile ranks (kept in registers)
-    uint32_t idx[KPT][KMAX], rnk[KPT][KMAX];
-    const uint64_t base = (uint64_t)blockIdx.x * (KPT * kBinThreads);
+    // phase 1: hash each key once; count its k indices per tile.  Only the index
+    // generator's start state (6 registers per key) is kept for phase 3.
+    IndexGen gen[KPT];
+    const uint64_t base = (uint64_t)blockIdx.x * (KPT * NT);
 #pragma unroll
     for (int p = 0; p < KPT; ++p) {
-        const uint64_t i = base + (uint64_t)p * kBinThreads + tid;
+        const uint64_t i = base + (uint64_t)p * NT + tid;
         if (i < n) {
             uint64_t h1, h2;
             hashes_of<FLAVOR, LAYOUT>(c, keys, offsets, key_len, i, &h1, &h2);
-            IndexGen g;
-            g.start(h1, h2, c);
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j) {
-                if ((uint32_t)j < c.k) {
-                    if (j) g.next(c);
-                    idx[p][j] = g.r;
-                    rnk[p][j] = atomicAdd(&hist[g.r >> tc.ts], 1u);
-                }
+            gen[p].start(h1, h2, c);
+            IndexGen g = gen[p];
+            for (uint32_t j = 0; j < c.k; ++j) {
+                if (j) g.next(c);
+                atomicAdd(&cnt[g.r >> tc.ts], 1u);
             }
         }
     }
     __syncthreads();
+    if (NB_DIAG_STOP(1)) return;
 
-    // phase 2: block-local run starts and global reservations
-    const uint32_t total = block_exclusive_scan(hist, S, T, wave_sums);
-    for (uint32_t t = tid; t < T; t += kBinThreads) {
-        const uint32_t h = hist[t];
-        G[t] = h ? atomicAdd(&gcur[t], h) : 0u;
+    // phase 2: block-local run starts; reserve a run in every touched tile's
+    // bucket shard (cursor shard = blockIdx % G, laid out [shard][tile])
+    const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
+    const uint32_t shard = blockIdx.x % tc.G;
+    uint32_t *cur = sc.gcur + (size_t)shard * T;
+    for (uint32_t t = tid; t < T; t += NT) {
+        const uint32_t h = cnt[t];
+        G[t] = h ? atomicAdd(&cur[t], h) : 0u;
+        cnt[t] = S[t];  // becomes the placement cursor
     }
     __syncthreads();
+    if (NB_DIAG_STOP(2)) return;
 
-    // phase 3: counting-sort the block's indices by tile
+    // phase 3: regenerate the indices and counting-sort them by tile
 #pragma unroll
     for (int p = 0; p < KPT; ++p) {
-        const uint64_t i = base + (uint64_t)p * kBinThreads + tid;
+        const uint64_t i = base + (uint64_t)p * NT + tid;
         if (i < n) {
-#pragma unroll
-            for (int j = 0; j < KMAX; ++j)
-                if ((uint32_t)j < c.k) sorted[S[idx[p][j] >> tc.ts] + rnk[p][j]] = idx[p][j];
+            IndexGen g = gen[p];
+            for (uint32_t j = 0; j < c.k; ++j) {
+                if (j) g.next(c);
+                sorted[atomicAdd(&cnt[g.r >> tc.ts], 1u)] = g.r;
+            }
         }
     }
     __syncthreads();
+    if (NB_DIAG_STOP(3)) return;
 
     // phase 4: coalesced write-out of the runs (spill beyond capacity)
-    for (uint32_t j = tid; j < total; j += kBinThreads) {
+    const uint32_t tmask = (1u << tc.ts) - 1;
+    for (uint32_t j = tid; j < total; j += NT) {
         const uint32_t v = sorted[j];
         const uint32_t t = v >> tc.ts;
         const uint32_t pos = G[t] + (j - S[t]);
-        if (pos < tc.cap)
-            buckets[(size_t)t * tc.cap + pos] = v;
-        else
-            __hip_atomic_fetch_or(words32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
+        if (pos < tc.cap) {
+            buckets[((size_t)t * tc.G + shard) * tc.cap + pos] =
+                (ENTRY)(sizeof(ENTRY) == 2 ? (v & tmask) : v);
+        } else {
+            __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
+            sc.spill_flag[t] = 1u;
+        }
     }
 }
 
-__global__ __launch_bounds__(kTileThreads) void bloom_tile_or_kernel(
-    TileCfg tc, uint32_t *__restrict__ gcur, const uint32_t *__restrict__ buckets,
-    uint64_t *__restrict__ words, uint64_t nwords) {
-    extern __shared__ uint32_t tile[];
+template <typename ENTRY, bool OVERWRITE, int NT = kTileThreads, int UNROLL = kTileUnroll>
+__global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
+    TileCfg tc, TileScratch sc, const ENTRY *__restrict__ buckets, uint64_t *__restrict__ words,
+    uint64_t nwords) {
+    extern __shared__ uint32_t tile[];  // [2^ts / 32] tile words, then 2*kShards+1 words
+    constexpr uint32_t kPerVec = 16 / sizeof(ENTRY);  // entries per 16-byte load
     const uint32_t t = blockIdx.x, tid = threadIdx.x;
     const uint32_t tile_words32 = 1u << (tc.ts - 5);
     const uint32_t mask = (1u << tc.ts) - 1;
-    for (uint32_t w = tid; w < tile_words32; w += kTileThreads) tile[w] = 0;
-    __syncthreads();
-    const uint32_t cnt = min(gcur[t], tc.cap);
-    const uint32_t *e = buckets + (size_t)t * tc.cap;
-    const uint4 *e4 = reinterpret_cast<const uint4 *>(e);
-    for (uint32_t q = tid; q < cnt / 4; q += kTileThreads) {
-        const uint4 v = e4[q];
-        atomicOr(&tile[(v.x & mask) >> 5], 1u << (v.x & 31));
-        atomicOr(&tile[(v.y & mask) >> 5], 1u << (v.y & 31));
-        atomicOr(&tile[(v.z & mask) >> 5], 1u << (v.z & 31));
-        atomicOr(&tile[(v.w & mask) >> 5], 1u << (v.w & 31));
-    }
-    for (uint32_t q = (cnt & ~3u) + tid; q < cnt; q += kTileThreads) {
-        const uint32_t v = e[q];
-        atomicOr(&tile[(v & mask) >> 5], 1u << (v & 31));
+    uint32_t *shard_cnt = tile + tile_words32;  // [kShards]
+    uint32_t *shard_v0 = shard_cnt + kShards;   // [kShards + 1] first flat vector of each shard
+    for (uint32_t w = tid; w < tile_words32; w += NT) tile[w] = 0;
+    if (tid < tc.G) {
+        uint32_t *cp = sc.gcur + (size_t)tid * tc.T + t;
+        shard_cnt[tid] = min(*cp, tc.cap);
+        *cp = 0;  // workspace invariant: cursors are zero between builds
     }
     __syncthreads();
-    if (tid == 0) gcur[t] = 0;  // the workspace invariant: cursors are zero between builds
+    if (tid == 0) {
+        uint32_t v0 = 0;
+        for (uint32_t g = 0; g < tc.G; ++g) {
+            shard_v0[g] = v0;
+            v0 += shard_cnt[g] / kPerVec;
+        }
+        shard_v0[tc.G] = v0;
+    }
+    __syncthreads();
+    auto orv = [&](uint32_t v) {
+        v &= mask;
+        atomicOr(&tile[v >> 5], 1u << (v & 31));
+    };
+    auto or_vec = [&](const uint4 &q) {
+        if (sizeof(ENTRY) == 2) {
+            orv(q.x & 0xffff); orv(q.x >> 16); orv(q.y & 0xffff); orv(q.y >> 16);
+            orv(q.z & 0xffff); orv(q.z >> 16); orv(q.w & 0xffff); orv(q.w >> 16);
+        } else {
+            orv(q.x); orv(q.y); orv(q.z); orv(q.w);
+        }
+    };
+    // the G shards as one flat range of 16-byte vectors
+    const ENTRY *tile_base = buckets + (size_t)t * tc.G * tc.cap;
+    const uint32_t nvec = shard_v0[tc.G];
+    auto vec_at = [&](uint32_t v) {
+        uint32_t g = 0;
+        while (g + 1 < tc.G && v >= shard_v0[g + 1]) ++g;
+        const uint4 *ev = reinterpret_cast<const uint4 *>(tile_base + (size_t)g * tc.cap);
+        return ev[v - shard_v0[g]];
+    };
+    uint32_t q = tid;
+    for (; q + (UNROLL - 1) * NT < nvec; q += UNROLL * NT) {
+        uint4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) v[u] = vec_at(q + u * NT);
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) or_vec(v[u]);
+    }
+    for (; q < nvec; q += NT) or_vec(vec_at(q));
+    if (tid < tc.G) {  // each shard's tail (< kPerVec entries)
+        const uint32_t cnt = shard_cnt[tid];
+        const ENTRY *e = tile_base + (size_t)tid * tc.cap;
+        for (uint32_t r = cnt / kPerVec * kPerVec; r < cnt; ++r) orv(e[r]);
+    }
     const uint64_t w0 = (uint64_t)t << (tc.ts - 6);
     const uint32_t tile_words64 = tile_words32 / 2;
+    if (sc.spill_flag[t]) {  // fold in (and clear) this tile's spilled bits
+        __syncthreads();
+        uint32_t *sp = sc.spill32 + 2 * w0;
+        for (uint32_t w = tid; w < tile_words32; w += NT) {
+            if ((w0 * 2 + w) < 2 * nwords) {
+                const uint32_t v = sp[w];
+                if (v) {
+                    atomicOr(&tile[w], v);
+                    sp[w] = 0;
+                }
+            }
+        }
+        if (tid == 0) sc.spill_flag[t] = 0;
+    }
+    __syncthreads();
     const uint64_t *tile64 = reinterpret_cast<const uint64_t *>(tile);
-    for (uint32_t w = tid; w < tile_words64; w += kTileThreads) {
+    for (uint32_t w = tid; w < tile_words64; w += NT) {
         const uint64_t gw = w0 + w;
         if (gw < nwords) {
             const uint64_t v = tile64[w];
-            if (v) words[gw] |= v;
+            if (OVERWRITE) words[gw] = v;
+            else if (v) words[gw] |= v;
         }
     }
 }
@@ -353,15 +438,16 @@ int check_common(uint64_t n, uint32_t m, int flavor, const void *keys, const voi
     return NB_OK;
 }
 
-// Per-(device, stream) scratch of the tiled path: tile cursors (kept zero between
-// builds by the tile kernel) and the bucket array.
+// Per-(device, stream) scratch of the tiled path: bucket cursors, spill flags and
+// the spill bitmap (all kept zero between builds by the tile kernel), and the
+// bucket array.
 struct Workspace {
     int dev = -1;
     hipStream_t st = nullptr;
-    uint32_t *gcur = nullptr;
-    size_t gcur_cap = 0;     // entries
-    uint32_t *buckets = nullptr;
-    size_t bucket_cap = 0;   // entries
+    uint32_t *zeroed = nullptr;   // gcur [kShards*kMaxTiles] | spill_flag [kMaxTiles] | spill32
+    size_t zeroed_bytes = 0;
+    void *buckets = nullptr;
+    size_t bucket_bytes = 0;
 };
 std::mutex g_ws_mu;
 std::vector<Workspace *> g_ws;
@@ -380,37 +466,58 @@ int get_ws(hipStream_t st, Workspace **out) {
     return NB_OK;
 }
 
-int ws_reserve(Workspace &w, uint32_t T, size_t entries) {
-    if (T > w.gcur_cap || entries > w.bucket_cap) NB_HIP(hipStreamSynchronize(w.st));
-    if (T > w.gcur_cap) {
-        if (w.gcur) NB_HIP(hipFree(w.gcur));
-        w.gcur = nullptr;
-        w.gcur_cap = 0;
-        const size_t want = std::max<size_t>(T, 4096);
-        NB_HIP(hipMalloc(&w.gcur, want * 4));
-        NB_HIP(hipMemset(w.gcur, 0, want * 4));
-        w.gcur_cap = want;
+constexpr size_t kCurWords = (size_t)kShards * kMaxTiles;
+
+// Grows the workspace (synchronising the stream before freeing old buffers).
+// Not graph-capturable when it has to grow: call once with the largest shape first.
+int ws_reserve(Workspace &w, uint32_t m, size_t bucket_bytes, TileScratch *sc) {
+    const size_t spill_words32 = 2 * (((size_t)m + 63) / 64);
+    const size_t zb = (kCurWords + kMaxTiles + spill_words32) * 4;
+    if (zb > w.zeroed_bytes || bucket_bytes > w.bucket_bytes) NB_HIP(hipStreamSynchronize(w.st));
+    if (zb > w.zeroed_bytes) {
+        if (w.zeroed) NB_HIP(hipFree(w.zeroed));
+        w.zeroed = nullptr;
+        w.zeroed_bytes = 0;
+        NB_HIP(hipMalloc(&w.zeroed, zb));
+        NB_HIP(hipMemset(w.zeroed, 0, zb));
+        w.zeroed_bytes = zb;
     }
-    if (entries > w.bucket_cap) {
+    if (bucket_bytes > w.bucket_bytes) {
         if (w.buckets) NB_HIP(hipFree(w.buckets));
         w.buckets = nullptr;
-        w.bucket_cap = 0;
-        const size_t want = entries + entries / 8;
-        NB_HIP(hipMalloc(&w.buckets, want * 4));
-        w.bucket_cap = want;
+        w.bucket_bytes = 0;
+        const size_t want = bucket_bytes + bucket_bytes / 8;
+        NB_HIP(hipMalloc(&w.buckets, want));
+        w.bucket_bytes = want;
     }
+    sc->gcur = w.zeroed;
+    sc->spill_flag = w.zeroed + kCurWords;
+    sc->spill32 = w.zeroed + kCurWords + kMaxTiles;
     return NB_OK;
 }
 
+uint32_t env_u32(const char *name, uint32_t dflt) {
+    const char *e = std::getenv(name);
+    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : dflt;
+}
+
+// Tile size policy (measured, tools/ubench_tiled.hip): 2^16-bit tiles with 16-bit
+// bucket entries while that needs <= 2048 tiles (m <= 2^27, e.g. C2); smaller
+// tiles for small m (>= ~1024 tiles, 2^12 bits minimum); above 2^27 bits the
+// smallest ts giving <= 2048 tiles (C3/C4: ts = 19), up to 2^20-bit tiles
+// (<= 4096 tiles at m = 2^32 - 1, C5) with 32-bit entries.
 TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     TileCfg tc;
-    uint32_t ts = 12;  // floor(log2(m / 256)) clamped to [12, 20]: >= 256 tiles when possible
-    while (ts < 20 && ((uint64_t)m >> (ts + 1)) >= 256) ++ts;
+    uint32_t ts = 12;
+    while (ts < 16 && ((uint64_t)m >> (ts + 1)) >= 1024) ++ts;
+    while (ts < 20 && (((uint64_t)m + (1ull << ts) - 1) >> ts) > 2048) ++ts;
+    ts = std::min<uint32_t>(std::max<uint32_t>(env_u32("NB_TILE_BITS", ts), 12), 20);
     tc.ts = ts;
     tc.T = (uint32_t)(((uint64_t)m + (1ull << ts) - 1) >> ts);
-    const double e = (double)n_chunk * k / tc.T;
+    tc.G = std::min<uint32_t>(std::max<uint32_t>(env_u32("NB_SHARDS", kShards), 1), kShards);
+    const double e = (double)n_chunk * k / ((double)tc.T * tc.G);
     uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
-    cap = (cap + 63) & ~63ull;
+    cap = (cap + 7) & ~7ull;
     tc.cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFC0ull);
     return tc;
 }
@@ -441,7 +548,8 @@ int allow_lds(K kernel, size_t bytes) {
 
 template <int FLAVOR, int LAYOUT>
 int launch_atomic(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
-                  const FilterConsts &c, uint64_t *words, hipStream_t st) {
+                  const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st) {
+    if (overwrite) NB_HIP(hipMemsetAsync(words, 0, (((size_t)c.fm.m + 63) / 64) * 8, st));
     hipLaunchKernelGGL((bloom_build_atomic_kernel<FLAVOR, LAYOUT>), dim3(grid_for(n)),
                        dim3(kBlock), 0, st, keys, offsets, key_len, n, c,
                        reinterpret_cast<uint32_t *>(words));
@@ -449,60 +557,79 @@ int launch_atomic(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len
     return NB_OK;
 }
 
-template <int FLAVOR, int LAYOUT, int KPT, int KMAX>
-int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
-                 const FilterConsts &c, uint64_t *words, hipStream_t st) {
+template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY>
+int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                   const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st,
+                   uint64_t chunk, const TileCfg &tc) {
     constexpr uint64_t kpb = (uint64_t)KPT * kBinThreads;
-    const uint64_t chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, chunk_keys()));
-    const TileCfg tc = choose_tiles(c.fm.m, chunk, c.k);
     Workspace *ws;
+    TileScratch sc;
     int rc;
     if ((rc = get_ws(st, &ws))) return rc;
-    if ((rc = ws_reserve(*ws, tc.T, (size_t)tc.T * tc.cap))) return rc;
+    if ((rc = ws_reserve(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * sizeof(ENTRY), &sc)))
+        return rc;
     const size_t bin_lds = (3ull * tc.T + 32 + kpb * c.k) * 4;
-    const size_t tile_lds = (size_t)1 << (tc.ts - 3);
-    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, KMAX>;
-    if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(bloom_tile_or_kernel, tile_lds))) return rc;
+    const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
+    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, ENTRY>;
+    auto tile_ow = bloom_tile_or_kernel<ENTRY, true>;
+    auto tile_or = bloom_tile_or_kernel<ENTRY, false>;
+    if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(tile_ow, tile_lds)) ||
+        (rc = allow_lds(tile_or, tile_lds)))
+        return rc;
     const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
-    uint32_t *w32 = reinterpret_cast<uint32_t *>(words);
+    ENTRY *bk = reinterpret_cast<ENTRY *>(ws->buckets);
     for (uint64_t done = 0; done < n; done += chunk) {
         const uint64_t cn = std::min(chunk, n - done);
         const uint8_t *ck = offsets ? keys : keys + done * key_len;
         const uint64_t *co = offsets ? offsets + done : nullptr;
         hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(kBinThreads), bin_lds,
-                           st, ck, co, key_len, cn, c, tc, ws->gcur, ws->buckets, w32);
+                           st, ck, co, key_len, cn, c, tc, sc, bk);
         NB_HIP(hipGetLastError());
-        hipLaunchKernelGGL(bloom_tile_or_kernel, dim3(tc.T), dim3(kTileThreads), tile_lds, st, tc,
-                           ws->gcur, ws->buckets, words, nwords);
+        hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(tc.T),
+                           dim3(kTileThreads), tile_lds, st, tc, sc, bk, words, nwords);
         NB_HIP(hipGetLastError());
     }
     return NB_OK;
 }
 
+template <int FLAVOR, int LAYOUT, int KPT>
+int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                 const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st) {
+    constexpr uint64_t kpb = (uint64_t)KPT * kBinThreads;
+    const uint64_t chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, chunk_keys()));
+    const TileCfg tc = choose_tiles(c.fm.m, chunk, c.k);
+    if (tc.ts <= 16 && env_u32("NB_ENTRY32", 0) == 0)
+        return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint16_t>(keys, offsets, key_len, n, c, words,
+                                                             overwrite, st, chunk, tc);
+    return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint32_t>(keys, offsets, key_len, n, c, words,
+                                                         overwrite, st, chunk, tc);
+}
+
 template <int FLAVOR, int LAYOUT>
 int launch_build_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
-                   const FilterConsts &c, uint64_t *words, hipStream_t st) {
+                   const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st) {
     BuildPath p = path_override();
-    if (p == BuildPath::kAuto) {
-        const TileCfg tc = choose_tiles(c.fm.m, n, c.k);
-        const bool ok = c.k <= 16 && tc.T <= 2048 && n >= 4096;
-        p = ok ? BuildPath::kTiled : BuildPath::kAtomic;
+    const bool tiled_ok = c.k <= 32 && choose_tiles(c.fm.m, 1, c.k).T <= kMaxTiles;
+    if (p == BuildPath::kAuto) p = (tiled_ok && n >= 4096) ? BuildPath::kTiled : BuildPath::kAtomic;
+    if (p == BuildPath::kTiled && tiled_ok) {
+        // keys per block sized so the block's sorted indices fit in LDS
+        if (c.k <= 8)
+            return launch_tiled<FLAVOR, LAYOUT, kBinKPT>(keys, offsets, key_len, n, c, words,
+                                                         overwrite, st);
+        return launch_tiled<FLAVOR, LAYOUT, 1>(keys, offsets, key_len, n, c, words, overwrite, st);
     }
-    if (p == BuildPath::kTiled && c.k <= 16 && choose_tiles(c.fm.m, 1, c.k).T <= 2048) {
-        if (c.k <= 8) return launch_tiled<FLAVOR, LAYOUT, 4, 8>(keys, offsets, key_len, n, c, words, st);
-        return launch_tiled<FLAVOR, LAYOUT, 2, 16>(keys, offsets, key_len, n, c, words, st);
-    }
-    return launch_atomic<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, st);
+    return launch_atomic<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, overwrite, st);
 }
 
 template <int FLAVOR>
 int launch_build_f(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
-                   const FilterConsts &c, uint64_t *words, hipStream_t st) {
+                   const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st) {
     if (!offsets && key_len == 16 && (reinterpret_cast<uintptr_t>(keys) & 15) == 0)
-        return launch_build_l<FLAVOR, kFixed16>(keys, offsets, key_len, n, c, words, st);
+        return launch_build_l<FLAVOR, kFixed16>(keys, offsets, key_len, n, c, words, overwrite, st);
     if (!offsets)
-        return launch_build_l<FLAVOR, kFixedStride>(keys, offsets, key_len, n, c, words, st);
-    return launch_build_l<FLAVOR, kOffsets>(keys, offsets, key_len, n, c, words, st);
+        return launch_build_l<FLAVOR, kFixedStride>(keys, offsets, key_len, n, c, words,
+                                                    overwrite, st);
+    return launch_build_l<FLAVOR, kOffsets>(keys, offsets, key_len, n, c, words, overwrite, st);
 }
 
 template <int FLAVOR>
@@ -525,12 +652,18 @@ int launch_probe_f(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
 
 int launch_build(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                  uint32_t m, uint32_t k, uint64_t seed, int flavor, uint64_t *words,
-                 hipStream_t st) {
-    if (n == 0 || k == 0) return NB_OK;
+                 bool overwrite, hipStream_t st) {
+    if (n == 0 || k == 0) {
+        if (overwrite && m) NB_HIP(hipMemsetAsync(words, 0, (((size_t)m + 63) / 64) * 8, st));
+        return NB_OK;
+    }
     FilterConsts c = nb::make_consts(m, k, seed, (uint32_t)flavor);
+    if (!offsets) nb::set_fixed_len(c, key_len);
     return flavor == NB_FLAVOR_MSVC_FNV1A
-               ? launch_build_f<NB_FLAVOR_MSVC_FNV1A>(keys, offsets, key_len, n, c, words, st)
-               : launch_build_f<NB_FLAVOR_LIBSTDCXX>(keys, offsets, key_len, n, c, words, st);
+               ? launch_build_f<NB_FLAVOR_MSVC_FNV1A>(keys, offsets, key_len, n, c, words,
+                                                      overwrite, st)
+               : launch_build_f<NB_FLAVOR_LIBSTDCXX>(keys, offsets, key_len, n, c, words,
+                                                     overwrite, st);
 }
 
 int launch_probe(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
@@ -542,6 +675,7 @@ int launch_probe(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
         return NB_OK;
     }
     FilterConsts c = nb::make_consts(m, k, seed, (uint32_t)flavor);
+    if (!offsets) nb::set_fixed_len(c, key_len);
     return flavor == NB_FLAVOR_MSVC_FNV1A
                ? launch_probe_f<NB_FLAVOR_MSVC_FNV1A>(keys, offsets, key_len, n, c, words, out, st)
                : launch_probe_f<NB_FLAVOR_LIBSTDCXX>(keys, offsets, key_len, n, c, words, out, st);
@@ -614,7 +748,7 @@ int nb_shutdown(void) {
         for (Workspace *w : g_ws) {
             (void)hipSetDevice(w->dev);
             (void)hipStreamSynchronize(w->st);
-            if (w->gcur) (void)hipFree(w->gcur);
+            if (w->zeroed) (void)hipFree(w->zeroed);
             if (w->buckets) (void)hipFree(w->buckets);
             delete w;
         }
@@ -668,7 +802,7 @@ int nb_build(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uin
         NB_HIP(hipMemcpyAsync(d->buf[1], offsets, (n + 1) * 8, hipMemcpyHostToDevice, d->stream));
     NB_HIP(hipMemcpyAsync(d->buf[2], words, wb, hipMemcpyHostToDevice, d->stream));
     rc = launch_build((const uint8_t *)d->buf[0], offsets ? (const uint64_t *)d->buf[1] : nullptr,
-                      key_len, n, m, k, h2_seed, flavor, (uint64_t *)d->buf[2], d->stream);
+                      key_len, n, m, k, h2_seed, flavor, (uint64_t *)d->buf[2], false, d->stream);
     if (rc) return rc;
     NB_HIP(hipMemcpyAsync(words, d->buf[2], wb, hipMemcpyDeviceToHost, d->stream));
     NB_HIP(hipStreamSynchronize(d->stream));
@@ -712,7 +846,19 @@ int nb_build_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t k
                     uint64_t *d_words, void *stream) {
     int rc = check_common(n, m, flavor, d_keys, d_words);
     if (rc) return rc;
-    return launch_build(d_keys, d_offsets, key_len, n, m, k, h2_seed, flavor, d_words,
+    return launch_build(d_keys, d_offsets, key_len, n, m, k, h2_seed, flavor, d_words, false,
+                        (hipStream_t)stream);
+}
+
+int nb_build_device_ex(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
+                       uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
+                       uint64_t *d_words, uint32_t flags, void *stream) {
+    if (flags & ~(uint32_t)NB_BUILD_OVERWRITE) return fail(NB_ERR_ARG, "unknown flags");
+    const bool overwrite = (flags & NB_BUILD_OVERWRITE) != 0;
+    if (overwrite && m && !d_words) return fail(NB_ERR_ARG, "NULL words");
+    int rc = check_common(n, m, flavor, d_keys, d_words);
+    if (rc) return rc;
+    return launch_build(d_keys, d_offsets, key_len, n, m, k, h2_seed, flavor, d_words, overwrite,
                         (hipStream_t)stream);
 }
 

@@ -111,6 +111,9 @@ struct FilterConsts {
     uint64_t pre_d[kMaxPrefixWords];  // libstdc++: pre-mixed whole prefix words
     uint64_t pre_tail;     // the r leftover prefix bytes, little-endian
     uint64_t fnv_pre;      // FNV-1a state after all D prefix bytes
+    uint64_t h2_init_fixed; // libstdc++ h2 state after the whole prefix words, for
+                            // keys of length fixed_len (fixed-length layouts only)
+    uint32_t fixed_len;
 };
 
 inline FilterConsts make_consts(uint32_t m, uint32_t k, uint64_t seed, uint32_t flavor) {
@@ -141,7 +144,22 @@ inline FilterConsts make_consts(uint32_t m, uint32_t k, uint64_t seed, uint32_t 
     uint64_t h = kFnvBasis;
     for (int i = 0; i < n; ++i) h = fnv_step(h, (uint8_t)dig[i]);
     c.fnv_pre = h;
+    c.fixed_len = 0;
+    c.h2_init_fixed = 0;
     return c;
+}
+
+// libstdc++ h2 state once the whole prefix words are mixed, for a key of `len`
+// bytes (the initial state depends on the total length len + D).
+inline uint64_t h2_state_after_prefix(const FilterConsts &c, uint64_t len) {
+    uint64_t g = kStdSeed ^ ((len + c.plen) * kMul);
+    for (uint32_t w = 0; w < c.pwords; ++w) g = (g ^ c.pre_d[w]) * kMul;
+    return g;
+}
+
+inline void set_fixed_len(FilterConsts &c, uint32_t len) {
+    c.fixed_len = len;
+    c.h2_init_fixed = h2_state_after_prefix(c, len);
 }
 
 
@@ -170,6 +188,13 @@ NB_HD void lsx_begin(const FilterConsts &c, LsxState &s, uint32_t len) {
     for (int w = 0; w < kMaxPrefixWords; ++w)
         if ((uint32_t)w < c.pwords) g = (g ^ c.pre_d[w]) * kMul;
     s.h2 = g;
+    s.kprev = c.prem ? c.pre_tail << (64 - 8 * c.prem) : 0;
+}
+
+// Same, with the h2 prefix state precomputed on the host (fixed-length keys).
+NB_HD void lsx_begin_fixed(const FilterConsts &c, LsxState &s, uint32_t len) {
+    s.h1 = lsx_init(len);
+    s.h2 = c.h2_init_fixed;
     s.kprev = c.prem ? c.pre_tail << (64 - 8 * c.prem) : 0;
 }
 
@@ -211,7 +236,7 @@ NB_HD void fnv_consume(uint64_t &h1, uint64_t &h2, uint64_t kw, int nbytes) {
 
 // Hash a key whose first byte sits at byte a (0..7) of aligned word Q(0);
 // Q(j) returns aligned word j.  Only words holding at least one key byte are read.
-template <int FLAVOR, class LoadQ>
+template <int FLAVOR, class LoadQ, bool FIXED_LEN = false>
 NB_HD void hash_aligned_words(const FilterConsts &c, LoadQ Q, uint32_t a, uint32_t len,
                               uint64_t *h1, uint64_t *h2) {
     const uint32_t nq = (a + len + 7) >> 3;
@@ -229,7 +254,8 @@ NB_HD void hash_aligned_words(const FilterConsts &c, LoadQ Q, uint32_t a, uint32
         *h2 = f2;
     } else {
         LsxState s;
-        lsx_begin(c, s, len);
+        if (FIXED_LEN) lsx_begin_fixed(c, s, len);
+        else lsx_begin(c, s, len);
         for (uint32_t j = 0; j < nk; ++j) {
             const uint64_t qnext = (j + 1 < nq) ? Q(j + 1) : 0;
             const uint64_t kw = mask_bytes(funnel(qcur, qnext, 8 * a), (int)(len - 8 * j));

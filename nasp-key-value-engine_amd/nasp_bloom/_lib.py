@@ -17,6 +17,8 @@ NB_ERR_HIP = -2
 NB_ERR_NODEV = -3
 NB_ERR_UNSUPPORTED = -4
 
+BUILD_OVERWRITE = 1
+
 FLAVOR_LIBSTDCXX = 0
 FLAVOR_MSVC_FNV1A = 1
 
@@ -36,6 +38,9 @@ _SIGS = {
                            C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p, C.c_int]),
     "nb_build_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
                                   C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p]),
+    "nb_build_device_ex": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
+                                     C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_uint32,
+                                     C.c_void_p]),
     "nb_probe_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
                                   C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p,
                                   C.c_void_p]),

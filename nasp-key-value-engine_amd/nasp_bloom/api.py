@@ -16,7 +16,7 @@ import time
 
 import numpy as np
 
-from ._lib import FLAVOR_LIBSTDCXX, NaspBloomError, check, lib
+from ._lib import BUILD_OVERWRITE, FLAVOR_LIBSTDCXX, NaspBloomError, check, lib
 
 
 def nwords(m: int) -> int:
@@ -53,15 +53,17 @@ def _check_device_args(keys, offsets, words):
 
 
 def build_device(keys, offsets, key_len: int, n: int, m: int, k: int, seed: int, flavor: int,
-                 words, stream=None) -> None:
-    """OR the k bits of n device-resident keys into `words` (int64/uint64 cuda tensor)."""
+                 words, stream=None, overwrite: bool = False) -> None:
+    """OR the k bits of n device-resident keys into `words` (int64/uint64 cuda tensor);
+    with overwrite=True, `words` becomes the filter of this batch alone."""
     _check_device_args(keys, offsets, words)
     if words.numel() * words.element_size() < nwords(m) * 8:
         raise NaspBloomError("words tensor smaller than ceil(m/64) u64 words")
-    rc = lib().nb_build_device(keys.data_ptr(), offsets.data_ptr() if offsets is not None else None,
-                               key_len, n, m, k, seed, flavor, words.data_ptr(),
-                               _stream_handle(stream))
-    check(rc, "nb_build_device")
+    rc = lib().nb_build_device_ex(keys.data_ptr(),
+                                  offsets.data_ptr() if offsets is not None else None,
+                                  key_len, n, m, k, seed, flavor, words.data_ptr(),
+                                  BUILD_OVERWRITE if overwrite else 0, _stream_handle(stream))
+    check(rc, "nb_build_device_ex")
 
 
 def probe_device(keys, offsets, key_len: int, n: int, m: int, k: int, seed: int, flavor: int,

@@ -64,6 +64,15 @@ int main() {
                 if (fl) nb::hash_aligned_words<1>(c, [q](uint32_t j) { return q[j]; }, a, (uint32_t)len, &g1, &g2);
                 else nb::hash_aligned_words<0>(c, [q](uint32_t j) { return q[j]; }, a, (uint32_t)len, &g1, &g2);
                 if (g1 != h1 || g2 != h2) ++hbad;
+                // fixed-length form: h2 prefix state precomputed on the host
+                nb::FilterConsts cf = c;
+                nb::set_fixed_len(cf, (uint32_t)len);
+                if (fl == 0) {
+                    auto load = [q](uint32_t j) { return q[j]; };
+                    nb::hash_aligned_words<0, decltype(load), true>(cf, load, a, (uint32_t)len,
+                                                                    &g1, &g2);
+                    if (g1 != h1 || g2 != h2) ++hbad;
+                }
                 for (uint32_t i = 0; i < 3; ++i) {
                     uint32_t want = orc_index(fl, buf, len, i, 1000003u, seed);
                     if ((uint32_t)((h1 + (uint64_t)i * h2) % 1000003u) != want) ++hbad;

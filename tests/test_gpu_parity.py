@@ -225,9 +225,9 @@ def test_empty_and_degenerate(dev, oracle, build_path):
     assert dev_probe(dev, np.zeros(48, np.uint8), None, 16, 3, 1000, 0, SEED, w0).tolist() == [1, 1, 1]
 
 
-@pytest.mark.parametrize("k", [1, 8, 9, 16, 17, 24])
+@pytest.mark.parametrize("k", [1, 8, 9, 16, 17, 24, 32, 33])
 def test_k_range_tiled(dev, oracle, k, monkeypatch):
-    """k selects the tiled kernel's register layout (<=8, <=16) or the atomic path (>16)."""
+    """k selects the tiled kernel's keys per block (<=8, <=16, <=32) or the atomic path (>32)."""
     from nasp_bloom import synth
     monkeypatch.setenv("NB_BUILD_PATH", "tiled")
     buf, offs = synth.var_keys(300_000, 4, 40)
@@ -261,6 +261,38 @@ def test_tiled_chunking(dev, oracle, chunk, monkeypatch):
     fixed = synth.fixed_keys(700_001, 16)
     got = dev_build(dev, fixed, None, 16, 700_001, 95_850_584, 7, SEED)
     np.testing.assert_array_equal(got, oracle.build(0, fixed, None, 16, 700_001, 95_850_584, 7, SEED))
+
+
+@pytest.mark.parametrize("path", ["atomic", "tiled"])
+def test_overwrite_mode(dev, oracle, path, monkeypatch):
+    """NB_BUILD_OVERWRITE: the words become the batch's filter whatever they held
+    before -- including when buckets spill (duplicated keys) and across chunks."""
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    monkeypatch.setenv("NB_BUILD_PATH", path)
+    m, k = 9_585_059, 7
+    buf, offs = synth.var_keys(500_000)
+    kt, ot = t_u8(buf, dev), t_u64(offs, dev)
+    stale = torch.full((nbm.nwords(m),), -1, dtype=torch.int64, device=dev)  # all ones
+    nbm.build_device(kt, ot, 0, 500_000, m, k, SEED, 0, stale, overwrite=True)
+    torch.cuda.synchronize()
+    want = oracle.build(0, buf, offs, 0, 500_000, m, k, SEED)
+    np.testing.assert_array_equal(stale.cpu().numpy().view(np.uint64), want)
+    # duplicated keys (spill path) into stale words, then a second chunked batch
+    dup = np.zeros(300_000 * 16 + 16, np.uint8)
+    dup[:16 * 500] = synth.fixed_keys(500, 16)[:16 * 500]
+    stale.fill_(-1)
+    monkeypatch.setenv("NB_CHUNK_KEYS", "70000")
+    nbm.build_device(t_u8(dup, dev), None, 16, 300_000, m, k, SEED, 0, stale, overwrite=True)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(stale.cpu().numpy().view(np.uint64),
+                                  oracle.build(0, dup, None, 16, 300_000, m, k, SEED))
+    # the spill bitmap and cursors were left clean: a normal build is exact again
+    fresh = torch.zeros(nbm.nwords(m), dtype=torch.int64, device=dev)
+    nbm.build_device(kt, ot, 0, 500_000, m, k, SEED, 0, fresh)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(fresh.cpu().numpy().view(np.uint64), want)
 
 
 def test_probe_parity(dev, oracle):

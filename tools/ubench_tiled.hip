@@ -1,0 +1,136 @@
+// ubench_tiled.hip -- diagnostic build of the tiled build path (not product code).
+// Includes the product kernels with NB_DIAG_STOP wired to a device constant, and
+// times, for the C2 workload (10M x 16B keys, m = 95,850,584, k = 7):
+//   * bin kernel configurations (keys/thread x threads/block) and tile sizes,
+//     each stopped after phase 1 / 2 / 3 / full, to price every phase;
+//   * tile kernel configurations (threads x loads in flight).
+#include <hip/hip_runtime.h>
+__constant__ int g_diag_stop;
+#define NB_DIAG_STOP(phase) (g_diag_stop == (phase))
+#include "../nasp-key-value-engine_amd/csrc/bloom_kernels.hip"
+
+#include <cstdio>
+
+#define CK(x)                                                               \
+    do {                                                                    \
+        hipError_t e = (x);                                                 \
+        if (e != hipSuccess) {                                              \
+            printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); \
+            exit(1);                                                        \
+        }                                                                   \
+    } while (0)
+
+__global__ void k_fill(uint64_t *p, uint64_t n) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+        uint64_t x = i + 0x9E3779B97F4A7C15ull;
+        x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+        x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+        p[i] = x ^ (x >> 31);
+    }
+}
+
+struct Ev {
+    hipEvent_t a, b;
+    Ev() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
+};
+
+static void set_stop(int s) { CK(hipMemcpyToSymbol(HIP_SYMBOL(g_diag_stop), &s, sizeof s)); }
+
+template <int KPT, typename E>
+static float time_bin(const uint8_t *keys, uint64_t n, const FilterConsts &c, TileCfg tc,
+                      TileScratch sc, void *buckets, int stop) {
+    constexpr int NT = kBinThreads;
+    constexpr uint64_t kpb = (uint64_t)KPT * NT;
+    const size_t lds = (3ull * tc.T + 32 + kpb * c.k) * 4;
+    auto kern = bloom_bin_kernel<0, kFixed16, KPT, E>;
+    if (lds > 160 * 1024) return -1.f;
+    allow_lds(kern, lds);
+    set_stop(stop);
+    Ev ev;
+    float best = 1e30f;
+    for (int r = 0; r < 3; ++r) {
+        CK(hipMemset(sc.gcur, 0, kCurWords * 4));
+        CK(hipEventRecord(ev.a));
+        hipLaunchKernelGGL(kern, dim3((uint32_t)((n + kpb - 1) / kpb)), dim3(NT), lds, 0, keys,
+                           nullptr, 16u, n, c, tc, sc, (E *)buckets);
+        CK(hipEventRecord(ev.b));
+        CK(hipEventSynchronize(ev.b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, ev.a, ev.b));
+        best = std::min(best, ms);
+    }
+    set_stop(0);
+    return best;
+}
+
+template <typename E, int UN>
+static float time_tile(const uint8_t *keys, uint64_t n, const FilterConsts &c, TileCfg tc,
+                       TileScratch sc, void *buckets, uint64_t *words) {
+    auto kern = bloom_tile_or_kernel<E, true, kTileThreads, UN>;
+    const size_t lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
+    allow_lds(kern, lds);
+    const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
+    Ev ev;
+    float best = 1e30f;
+    for (int r = 0; r < 3; ++r) {
+        time_bin<kBinKPT, E>(keys, n, c, tc, sc, buckets, 0);
+        CK(hipEventRecord(ev.a));
+        hipLaunchKernelGGL(kern, dim3(tc.T), dim3(kTileThreads), lds, 0, tc, sc, (const E *)buckets,
+                           words, nwords);
+        CK(hipEventRecord(ev.b));
+        CK(hipEventSynchronize(ev.b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, ev.a, ev.b));
+        best = std::min(best, ms);
+    }
+    return best;
+}
+
+int main() {
+    const uint64_t n = 10000000;
+    const uint32_t m = 95850584, k = 7;
+    uint8_t *keys;
+    uint64_t *words;
+    CK(hipMalloc(&keys, n * 16 + 64));
+    CK(hipMalloc(&words, ((uint64_t)m + 63) / 64 * 8));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint64_t *>(keys), 2 * n);
+    FilterConsts c = nb::make_consts(m, k, 17027509906831645879ull, 0);
+    nb::set_fixed_len(c, 16);
+    void *buckets;
+    TileScratch sc;
+    uint32_t *zeroed;
+    const size_t zb = (kCurWords + kMaxTiles + 2 * (((size_t)m + 63) / 64)) * 4;
+    CK(hipMalloc(&zeroed, zb));
+    CK(hipMemset(zeroed, 0, zb));
+    sc.gcur = zeroed;
+    sc.spill_flag = zeroed + kCurWords;
+    sc.spill32 = zeroed + kCurWords + kMaxTiles;
+    CK(hipMalloc(&buckets, (size_t)n * k * 4 * 2 + (1 << 26)));
+    for (uint32_t ts : {15u, 16u, 17u}) {
+        for (uint32_t G : {1u, 4u, 8u}) {
+            TileCfg tc;
+            tc.ts = ts;
+            tc.T = (uint32_t)(((uint64_t)m + (1ull << ts) - 1) >> ts);
+            tc.G = G;
+            double e = (double)n * k / ((double)tc.T * G);
+            tc.cap = ((uint32_t)(e + 8 * std::sqrt(e) + 64) + 7) & ~7u;
+            printf("ts=%u T=%u G=%u cap=%u\n", ts, tc.T, G, tc.cap);
+#define BIN(KPT, E)                                                                          \
+    printf("  bin KPT=%d %s  p1 %.4f  p12 %.4f  p123 %.4f  full %.4f ms\n", KPT, #E,         \
+           time_bin<KPT, E>(keys, n, c, tc, sc, buckets, 1),                          \
+           time_bin<KPT, E>(keys, n, c, tc, sc, buckets, 2),                          \
+           time_bin<KPT, E>(keys, n, c, tc, sc, buckets, 3),                          \
+           time_bin<KPT, E>(keys, n, c, tc, sc, buckets, 0));
+            BIN(1, uint32_t);
+            BIN(2, uint32_t);
+            if (ts <= 16) BIN(2, uint16_t);
+#define TILE(E, UN) \
+    printf("  tile %s UNROLL=%d  %.4f ms\n", #E, UN, time_tile<E, UN>(keys, n, c, tc, sc, buckets, words));
+            TILE(uint32_t, 1);
+            TILE(uint32_t, 2);
+            if (ts <= 16) { TILE(uint16_t, 1); TILE(uint16_t, 2); }
+        }
+    }
+    CK(hipDeviceSynchronize());
+    return 0;
+}
