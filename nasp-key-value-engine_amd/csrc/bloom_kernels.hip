@@ -53,9 +53,8 @@ __device__ __forceinline__ void key_hashes_ptr(const FilterConsts &c, const uint
 
 // Fixed 16-byte keys, 16-byte aligned: one dwordx4 load per lane.
 template <int FLAVOR>
-__device__ __forceinline__ void key_hashes_16(const FilterConsts &c, const uint8_t *keys,
-                                              uint64_t i, uint64_t *h1, uint64_t *h2) {
-    const ulonglong2 kv = reinterpret_cast<const ulonglong2 *>(keys)[i];
+__device__ __forceinline__ void hash16(const FilterConsts &c, const ulonglong2 &kv, uint64_t *h1,
+                                       uint64_t *h2) {
     if (FLAVOR == NB_FLAVOR_MSVC_FNV1A) {
         uint64_t f1 = nb::kFnvBasis, f2 = c.fnv_pre;
         nb::fnv_consume(f1, f2, kv.x, 8);
@@ -70,6 +69,40 @@ __device__ __forceinline__ void key_hashes_16(const FilterConsts &c, const uint8
         nb::lsx_end(c, s, 16, h1, h2);
     }
 }
+
+template <int FLAVOR>
+__device__ __forceinline__ void key_hashes_16(const FilterConsts &c, const uint8_t *keys,
+                                              uint64_t i, uint64_t *h1, uint64_t *h2) {
+    hash16<FLAVOR>(c, reinterpret_cast<const ulonglong2 *>(keys)[i], h1, h2);
+}
+
+// A block's KPT keys per lane: all loads issued before any hashing, so a lane
+// has KPT key loads (fixed 16-byte keys) or offset pairs (variable keys) in
+// flight at once instead of one exposed latency per key.
+template <int FLAVOR, int LAYOUT, int KPT>
+struct KeyBatch {
+    ulonglong2 kv[KPT];
+    uint64_t b[KPT], e[KPT];
+    __device__ __forceinline__ void load(const uint8_t *keys, const uint64_t *offsets,
+                                         uint64_t base, uint64_t stride, uint64_t n) {
+#pragma unroll
+        for (int p = 0; p < KPT; ++p) {
+            const uint64_t i = base + p * stride;
+            if (i < n) {
+                if (LAYOUT == kFixed16) kv[p] = reinterpret_cast<const ulonglong2 *>(keys)[i];
+                else if (LAYOUT == kOffsets) { b[p] = offsets[i]; e[p] = offsets[i + 1]; }
+            }
+        }
+    }
+    __device__ __forceinline__ void hash(const FilterConsts &c, const uint8_t *keys,
+                                         uint32_t key_len, uint64_t i, int p, uint64_t *h1,
+                                         uint64_t *h2) const {
+        if (LAYOUT == kFixed16) hash16<FLAVOR>(c, kv[p], h1, h2);
+        else if (LAYOUT == kFixedStride)
+            key_hashes_ptr<FLAVOR, true>(c, keys + i * key_len, key_len, h1, h2);
+        else key_hashes_ptr<FLAVOR, false>(c, keys + b[p], (uint32_t)(e[p] - b[p]), h1, h2);
+    }
+};
 
 template <int FLAVOR, int LAYOUT>
 __device__ __forceinline__ void hashes_of(const FilterConsts &c, const uint8_t *keys,
@@ -173,12 +206,16 @@ constexpr int kBinKPT = 2;       // keys per thread when k <= 8 (1 for larger k)
 constexpr int kTileThreads = 1024;
 constexpr int kTileUnroll = 2;   // 16-byte bucket loads in flight per lane
 constexpr int kShards = 8;
+constexpr uint32_t kStageBytes = 48 * 1024;  // LDS staging window for variable-length keys
 constexpr uint32_t kMaxTiles = 4096;
 
 // Diagnostic builds (tools/ubench_tiled.hip) stop a kernel after a phase to price
 // it; in the product this is compiled out.
 #ifndef NB_DIAG_STOP
 #define NB_DIAG_STOP(phase) false
+#endif
+#ifndef NB_DIAG_PROLOGUE
+#define NB_DIAG_PROLOGUE()
 #endif
 
 // Exclusive scan of hist[0..T) into S[0..T); returns the total.  blockDim = NT.
@@ -219,13 +256,21 @@ __device__ uint32_t block_exclusive_scan(const uint32_t *hist, uint32_t *S, uint
     return wave_sums[kWaves];
 }
 
+// LDS carve of the bin kernel: cnt | S | G | wave_sums[32] | sort/stage area,
+// the last one 16-byte aligned (Guideline 17: misaligned b64/b128 LDS accesses
+// replay at 64 cycles per wave-instruction).
+__host__ __device__ constexpr uint32_t bin_sort_offset_words(uint32_t T) {
+    return (3 * T + 32 + 3) & ~3u;
+}
+
 struct TileScratch {
     uint32_t *gcur;       // [G][T] bucket cursors (zero between builds)
     uint32_t *spill_flag; // [T]    (zero between builds)
     uint32_t *spill32;    // [2*ceil(m/64)] spill bitmap (zero between builds)
 };
 
-template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY, int NT = kBinThreads>
+template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY, int NT = kBinThreads,
+          bool STAGE = (LAYOUT != kFixed16)>
 __global__ __launch_bounds__(NT) void bloom_bin_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
     uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc, ENTRY *__restrict__ buckets) {
@@ -235,8 +280,9 @@ __global__ __launch_bounds__(NT) void bloom_bin_kernel(
     uint32_t *S = cnt + T;             // [T] block-local run starts
     uint32_t *G = S + T;               // [T] bucket positions of the runs
     uint32_t *wave_sums = G + T;       // [NT/64 + 1]
-    uint32_t *sorted = wave_sums + 32; // [KPB * k]
+    uint32_t *sorted = lds + bin_sort_offset_words(T);  // [KPB * k], 16-byte aligned
     const uint32_t tid = threadIdx.x;
+    NB_DIAG_PROLOGUE();
     for (uint32_t t = tid; t < T; t += NT) cnt[t] = 0;
     __syncthreads();
 
@@ -244,17 +290,69 @@ __global__ __launch_bounds__(NT) void bloom_bin_kernel(
     // generator's start state (6 registers per key) is kept for phase 3.
     IndexGen gen[KPT];
     const uint64_t base = (uint64_t)blockIdx.x * (KPT * NT);
+    auto count_key = [&](int p, uint64_t h1, uint64_t h2) {
+        gen[p].start(h1, h2, c);
+        IndexGen g = gen[p];
+        for (uint32_t j = 0; j < c.k; ++j) {
+            if (j) g.next(c);
+            atomicAdd(&cnt[g.r >> tc.ts], 1u);
+        }
+    };
+    if (!STAGE) {
+        KeyBatch<FLAVOR, LAYOUT, KPT> kb;
+        kb.load(keys, offsets, base + tid, NT, n);
 #pragma unroll
-    for (int p = 0; p < KPT; ++p) {
-        const uint64_t i = base + (uint64_t)p * NT + tid;
-        if (i < n) {
-            uint64_t h1, h2;
-            hashes_of<FLAVOR, LAYOUT>(c, keys, offsets, key_len, i, &h1, &h2);
-            gen[p].start(h1, h2, c);
-            IndexGen g = gen[p];
-            for (uint32_t j = 0; j < c.k; ++j) {
-                if (j) g.next(c);
-                atomicAdd(&cnt[g.r >> tc.ts], 1u);
+        for (int p = 0; p < KPT; ++p) {
+            const uint64_t i = base + (uint64_t)p * NT + tid;
+            if (i < n) {
+                uint64_t h1, h2;
+                kb.hash(c, keys, key_len, i, p, &h1, &h2);
+                count_key(p, h1, h2);
+            }
+        }
+    } else {
+        // Variable-length (or odd fixed-length) keys: the block's keys are one
+        // contiguous byte range.  When it fits the stage (the not-yet-used sort
+        // array) it is loaded into LDS with coalesced 16-byte loads and every key
+        // is hashed from LDS; otherwise (very long keys) the lanes read HBM.
+        uint8_t *stage = reinterpret_cast<uint8_t *>(sorted);
+        const uint64_t blk_end = min(base + (uint64_t)KPT * NT, n);
+        auto koff = [&](uint64_t i) -> uint64_t {
+            return LAYOUT == kOffsets ? offsets[i] : i * (uint64_t)key_len;
+        };
+        uint64_t b[KPT], e[KPT];
+#pragma unroll
+        for (int p = 0; p < KPT; ++p) {
+            const uint64_t i = base + (uint64_t)p * NT + tid;
+            b[p] = e[p] = 0;
+            if (i < n) { b[p] = koff(i); e[p] = koff(i + 1); }
+        }
+        const uint64_t wb = koff(base) & ~15ull;
+        const uint64_t span = koff(blk_end) - wb;
+        const bool staged = span <= (uint64_t)kStageBytes;  // block-uniform
+        if (staged) {
+            const uint4 *src = reinterpret_cast<const uint4 *>(keys + wb);
+            uint4 *dst = reinterpret_cast<uint4 *>(stage);
+            const uint32_t nvec = (uint32_t)((span + 15) / 16);
+            for (uint32_t q = tid; q < nvec; q += NT) dst[q] = src[q];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < KPT; ++p) {
+            const uint64_t i = base + (uint64_t)p * NT + tid;
+            if (i < n) {
+                uint64_t h1, h2;
+                const uint32_t len = (uint32_t)(e[p] - b[p]);
+                if (staged) {
+                    const uint32_t lo = (uint32_t)(b[p] - wb), a = lo & 7u;
+                    const uint64_t *q = reinterpret_cast<const uint64_t *>(stage + (lo - a));
+                    auto load = [q](uint32_t j) { return q[j]; };
+                    nb::hash_aligned_words<FLAVOR, decltype(load), LAYOUT == kFixedStride>(
+                        c, load, a, len, &h1, &h2);
+                } else {
+                    key_hashes_ptr<FLAVOR, LAYOUT == kFixedStride>(c, keys + b[p], len, &h1, &h2);
+                }
+                count_key(p, h1, h2);
             }
         }
     }
@@ -557,20 +655,22 @@ int launch_atomic(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len
     return NB_OK;
 }
 
-template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY>
+template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY, int NT, bool STAGE>
 int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                    const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st,
                    uint64_t chunk, const TileCfg &tc) {
-    constexpr uint64_t kpb = (uint64_t)KPT * kBinThreads;
+    constexpr uint64_t kpb = (uint64_t)KPT * NT;
     Workspace *ws;
     TileScratch sc;
     int rc;
     if ((rc = get_ws(st, &ws))) return rc;
     if ((rc = ws_reserve(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * sizeof(ENTRY), &sc)))
         return rc;
-    const size_t bin_lds = (3ull * tc.T + 32 + kpb * c.k) * 4;
+    size_t sort_bytes = kpb * c.k * 4;
+    if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, kStageBytes);
+    const size_t bin_lds = (size_t)bin_sort_offset_words(tc.T) * 4 + sort_bytes;
     const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
-    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, ENTRY>;
+    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, ENTRY, NT, STAGE>;
     auto tile_ow = bloom_tile_or_kernel<ENTRY, true>;
     auto tile_or = bloom_tile_or_kernel<ENTRY, false>;
     if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(tile_ow, tile_lds)) ||
@@ -582,7 +682,7 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         const uint64_t cn = std::min(chunk, n - done);
         const uint8_t *ck = offsets ? keys : keys + done * key_len;
         const uint64_t *co = offsets ? offsets + done : nullptr;
-        hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(kBinThreads), bin_lds,
+        hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds,
                            st, ck, co, key_len, cn, c, tc, sc, bk);
         NB_HIP(hipGetLastError());
         hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(tc.T),
@@ -592,17 +692,17 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     return NB_OK;
 }
 
-template <int FLAVOR, int LAYOUT, int KPT>
+template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE>
 int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                  const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st) {
-    constexpr uint64_t kpb = (uint64_t)KPT * kBinThreads;
+    constexpr uint64_t kpb = (uint64_t)KPT * NT;
     const uint64_t chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, chunk_keys()));
     const TileCfg tc = choose_tiles(c.fm.m, chunk, c.k);
     if (tc.ts <= 16 && env_u32("NB_ENTRY32", 0) == 0)
-        return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint16_t>(keys, offsets, key_len, n, c, words,
-                                                             overwrite, st, chunk, tc);
-    return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint32_t>(keys, offsets, key_len, n, c, words,
-                                                         overwrite, st, chunk, tc);
+        return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint16_t, NT, STAGE>(
+            keys, offsets, key_len, n, c, words, overwrite, st, chunk, tc);
+    return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint32_t, NT, STAGE>(
+        keys, offsets, key_len, n, c, words, overwrite, st, chunk, tc);
 }
 
 template <int FLAVOR, int LAYOUT>
@@ -613,10 +713,24 @@ int launch_build_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     if (p == BuildPath::kAuto) p = (tiled_ok && n >= 4096) ? BuildPath::kTiled : BuildPath::kAtomic;
     if (p == BuildPath::kTiled && tiled_ok) {
         // keys per block sized so the block's sorted indices fit in LDS
-        if (c.k <= 8)
-            return launch_tiled<FLAVOR, LAYOUT, kBinKPT>(keys, offsets, key_len, n, c, words,
-                                                         overwrite, st);
-        return launch_tiled<FLAVOR, LAYOUT, 1>(keys, offsets, key_len, n, c, words, overwrite, st);
+        if (LAYOUT == kFixed16) {
+            if (c.k <= 8)
+                return launch_tiled<FLAVOR, LAYOUT, kBinKPT, kBinThreads, false>(
+                    keys, offsets, key_len, n, c, words, overwrite, st);
+            return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, false>(keys, offsets, key_len, n,
+                                                                       c, words, overwrite, st);
+        }
+        // variable-length keys: LDS-staged reads (default) or per-lane HBM reads
+        // (NB_VAR_MODE=0, kept for A/B: equal speed on C3, tools/varmode_gpu.sh)
+        if (env_u32("NB_VAR_MODE", 2) == 0) {
+            if (c.k <= 8)
+                return launch_tiled<FLAVOR, LAYOUT, 2, kBinThreads, false>(
+                    keys, offsets, key_len, n, c, words, overwrite, st);
+            return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, false>(keys, offsets, key_len, n,
+                                                                       c, words, overwrite, st);
+        }
+        return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, true>(keys, offsets, key_len, n, c,
+                                                                  words, overwrite, st);
     }
     return launch_atomic<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, overwrite, st);
 }

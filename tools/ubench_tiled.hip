@@ -7,6 +7,16 @@
 #include <hip/hip_runtime.h>
 __constant__ int g_diag_stop;
 #define NB_DIAG_STOP(phase) (g_diag_stop == (phase))
+__constant__ int g_stagger_blocks;  // blocks [lo, 2*lo) sleep ~g_stagger_cycles at start
+__constant__ int g_stagger_cycles;
+#define NB_DIAG_PROLOGUE()                                                              \
+    do {                                                                                \
+        if (g_stagger_blocks && blockIdx.x >= (unsigned)g_stagger_blocks &&             \
+            blockIdx.x < 2u * g_stagger_blocks) {                                       \
+            const long long t0 = clock64();                                             \
+            while (clock64() - t0 < g_stagger_cycles) __builtin_amdgcn_s_sleep(8);      \
+        }                                                                               \
+    } while (0)
 #include "../nasp-key-value-engine_amd/csrc/bloom_kernels.hip"
 
 #include <cstdio>
@@ -35,6 +45,10 @@ struct Ev {
 };
 
 static void set_stop(int s) { CK(hipMemcpyToSymbol(HIP_SYMBOL(g_diag_stop), &s, sizeof s)); }
+static void set_stagger(int blocks, int cycles) {
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stagger_blocks), &blocks, sizeof blocks));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stagger_cycles), &cycles, sizeof cycles));
+}
 
 template <int KPT, typename E>
 static float time_bin(const uint8_t *keys, uint64_t n, const FilterConsts &c, TileCfg tc,
@@ -106,30 +120,22 @@ int main() {
     sc.spill_flag = zeroed + kCurWords;
     sc.spill32 = zeroed + kCurWords + kMaxTiles;
     CK(hipMalloc(&buckets, (size_t)n * k * 4 * 2 + (1 << 26)));
-    for (uint32_t ts : {15u, 16u, 17u}) {
-        for (uint32_t G : {1u, 4u, 8u}) {
-            TileCfg tc;
-            tc.ts = ts;
-            tc.T = (uint32_t)(((uint64_t)m + (1ull << ts) - 1) >> ts);
-            tc.G = G;
-            double e = (double)n * k / ((double)tc.T * G);
-            tc.cap = ((uint32_t)(e + 8 * std::sqrt(e) + 64) + 7) & ~7u;
-            printf("ts=%u T=%u G=%u cap=%u\n", ts, tc.T, G, tc.cap);
-#define BIN(KPT, E)                                                                          \
-    printf("  bin KPT=%d %s  p1 %.4f  p12 %.4f  p123 %.4f  full %.4f ms\n", KPT, #E,         \
-           time_bin<KPT, E>(keys, n, c, tc, sc, buckets, 1),                          \
-           time_bin<KPT, E>(keys, n, c, tc, sc, buckets, 2),                          \
-           time_bin<KPT, E>(keys, n, c, tc, sc, buckets, 3),                          \
-           time_bin<KPT, E>(keys, n, c, tc, sc, buckets, 0));
-            BIN(1, uint32_t);
-            BIN(2, uint32_t);
-            if (ts <= 16) BIN(2, uint16_t);
-#define TILE(E, UN) \
-    printf("  tile %s UNROLL=%d  %.4f ms\n", #E, UN, time_tile<E, UN>(keys, n, c, tc, sc, buckets, words));
-            TILE(uint32_t, 1);
-            TILE(uint32_t, 2);
-            if (ts <= 16) { TILE(uint16_t, 1); TILE(uint16_t, 2); }
-        }
+    {
+        TileCfg tc;
+        tc.ts = 16;
+        tc.T = (uint32_t)(((uint64_t)m + (1ull << 16) - 1) >> 16);
+        tc.G = 8;
+        double e = (double)n * k / ((double)tc.T * tc.G);
+        tc.cap = ((uint32_t)(e + 8 * std::sqrt(e) + 64) + 7) & ~7u;
+        printf("ts=16 T=%u G=8 stagger sweep (full bin kernel, u16)\n", tc.T);
+        for (int sb : {0, 256, 128, 512})
+            for (int cyc : {2000, 8000, 20000, 40000}) {
+                set_stagger(sb, cyc);
+                printf("  stagger blocks [%d,%d) cycles %6d : %.4f ms\n", sb, 2 * sb, cyc,
+                       time_bin<kBinKPT, uint16_t>(keys, n, c, tc, sc, buckets, 0));
+                if (!sb) break;
+            }
+        set_stagger(0, 0);
     }
     CK(hipDeviceSynchronize());
     return 0;
