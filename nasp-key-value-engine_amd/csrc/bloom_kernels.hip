@@ -630,10 +630,15 @@ BuildPath path_override() {
     return BuildPath::kAuto;
 }
 
-uint64_t chunk_keys() {
+// Keys per bin/tile pass: the whole batch while its buckets stay under ~8 GB of
+// HBM (one pass over the filter), else equal chunks under that budget.
+uint64_t chunk_keys(uint64_t n, uint32_t k) {
     const char *e = std::getenv("NB_CHUNK_KEYS");
-    uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
-    return v ? v : (1ull << 27);
+    const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
+    if (v) return v;
+    const uint64_t budget = (8ull << 30) / (4ull * std::max<uint32_t>(k, 1));  // keys
+    const uint64_t passes = (n + budget - 1) / budget;
+    return std::max<uint64_t>(1, (n + passes - 1) / std::max<uint64_t>(passes, 1));
 }
 
 template <class K>
@@ -696,7 +701,7 @@ template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE>
 int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                  const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st) {
     constexpr uint64_t kpb = (uint64_t)KPT * NT;
-    const uint64_t chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, chunk_keys()));
+    const uint64_t chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, chunk_keys(n, c.k)));
     const TileCfg tc = choose_tiles(c.fm.m, chunk, c.k);
     if (tc.ts <= 16 && env_u32("NB_ENTRY32", 0) == 0)
         return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint16_t, NT, STAGE>(

@@ -1,0 +1,86 @@
+// BloomFilter.h -- drop-in replacement for the reference class
+// (reference BloomFilter/BloomFilter.h:12-42), backed by the MI355X build path.
+//
+// Same public surface, argument meaning and semantics, so the reference callers
+// compile unchanged: SSTable::build (SSTable/SSTable.cpp:28-35), the Raw/Comp
+// filter writers and readers (SSTableRaw.cpp:539,620; SSTableComp.cpp:476,555),
+// TypesManager (System/TypesManager.cpp:58-107).
+//
+// What changes inside:
+//   - the bit set is a std::vector<uint64_t> (little-endian words == the
+//     serialized LSB-first byte image) instead of vector<bool>;
+//   - add() appends the key to a packed batch (bytes + offsets); the batch is
+//     built on the GPU in one call (nb_build, include/nasp_bloom.h) when the
+//     filter is next read (possiblyContains / serialize / copy) or when it grows
+//     past kBatchKeys;
+//   - possiblyContains() of one key is evaluated on the host against the same
+//     bits (the latency-bound lookup path, SSTManager.cpp:203,224), with the
+//     exact same index arithmetic the kernels use (csrc/bloom_math.h).
+// Semantics kept: default-constructed filter answers true for every key
+// (BloomFilter.cpp:26,67-80); add() after deserialize() ORs into the loaded bits
+// (TypesManager.cpp:84-86); serialize() is byte-identical (BloomFilter.cpp:88-129).
+//
+// A failed device build throws std::runtime_error: there is no CPU fallback.
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+#include <vector>
+
+class BloomFilter {
+private:
+    unsigned int m = 0;         // Size of the bit set/array
+    unsigned int k = 0;         // Number of hash functions
+    double p = 0.0;             // False-positive probability
+    mutable std::vector<uint64_t> bits;  // Bit set: ceil(m/64) little-endian words
+                                         // (mutable: const readers build pending keys)
+    unsigned int timeConst = 0; // Seed for generating hash functions
+    size_t h2_seed = 0;         // Seed for the second hash function
+    bool closures = false;      // the reference's hashFunctions is non-empty
+
+    int flavor;                 // std::hash flavour (NB_FLAVOR_*)
+    int device = 0;
+    // pending batch of added keys (materialised lazily; mutable for const readers)
+    mutable std::vector<uint8_t> pend_bytes;
+    mutable std::vector<uint64_t> pend_offs;  // n+1 offsets (empty when no keys)
+
+    void flush() const;
+
+public:
+    static constexpr size_t kBatchKeys = size_t(1) << 22;
+
+    // Constructor
+    BloomFilter();
+    BloomFilter(unsigned int n, double falsePositiveRate);
+
+    // Add an element to the Bloom Filter
+    void add(const std::string& elem);
+
+    // Check if an element is present
+    bool possiblyContains(const std::string& elem) const;
+
+    // Serialize Bloom Filter to a vector of bytes
+    std::vector<std::byte> serialize() const;
+
+    // Deserialize Bloom Filter from a vector of bytes
+    static BloomFilter deserialize(const std::vector<std::byte>& data);
+
+    // Helper functions
+    static unsigned int calculateSizeOfBitSet(unsigned int expectedElements, double falsePositiveRate);
+    static unsigned int calculateNumberOfHashFunctions(unsigned int expectedElements, unsigned int m);
+
+    // ---- extensions (not in the reference) ----
+    // Which std::hash the filter's indices follow: NB_FLAVOR_LIBSTDCXX (default,
+    // a Linux build of the reference) or NB_FLAVOR_MSVC_FNV1A (files written by
+    // the authors' Windows build, e.g. the reference's committed *.sst filters).
+    static void setDefaultFlavor(int flavor);
+    void setFlavor(int f) { flush(); flavor = f; }
+    void setDevice(int d) { device = d; }
+    // Add many keys at once (same result as add() on each).
+    void addBatch(const std::vector<std::string>& elems);
+    // Build every pending key now (no-op if none).
+    void materialize() const { flush(); }
+    unsigned int bitCount() const { return m; }
+    unsigned int hashCount() const { return k; }
+};

@@ -1,0 +1,96 @@
+"""Multi-GPU builds over torch.distributed (backend "nccl" = RCCL over xGMI).
+
+Two shapes:
+
+* Independent filters (C4, the compaction fan-out): every rank builds its own
+  SSTable's filter from its own keys.  No collective on the data path -- see
+  `build_independent`.
+
+* One cooperative filter (C5, 1B keys into m = 2^32-1 bits): keys are split into
+  contiguous ranges, one per rank; each rank builds a full-size partial filter
+  from its range (the OR of the partial filters is exactly the filter of all
+  keys, because a Bloom filter is an OR of its keys' bits).  RCCL has no bitwise-
+  OR reduction (ncclRedOp_t is sum/prod/max/min/avg), so the merge is a
+  reduce-scatter built by hand: one all-to-all of equal word slices (rank j
+  receives slice j of every partial; over the xGMI full mesh each peer pair uses
+  its own link, (W-1)/W of the filter per rank instead of a ring's 2(W-1)/W over
+  one link), then a local W-way OR kernel (nb_or_merge_device) into the owned
+  slice, then optionally an all-gather of the owned slices so every rank holds
+  the whole filter.
+
+The collective logic takes its build/merge steps as parameters so the same code
+is exercised by world-size-2 gloo tests on CPU (tests/test_distributed.py, with
+the oracle as the test-side builder); on the GPU the defaults are the HIP kernels.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+import torch.distributed as dist
+
+from .api import build_device, nwords, or_merge_device
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous key range [begin, end) of `rank` (sizes differ by at most 1)."""
+    q, r = divmod(n, world)
+    begin = rank * q + min(rank, r)
+    return begin, begin + q + (1 if rank < r else 0)
+
+
+def slice_words(m: int, world: int) -> int:
+    """Words per rank slice (the filter's ceil(m/64) words padded to world*S)."""
+    nw = nwords(m)
+    return (nw + world - 1) // world
+
+
+def _hip_merge(dst: torch.Tensor, recv: torch.Tensor, nsrc: int, stride: int) -> None:
+    or_merge_device(dst, recv, dst.numel(), nsrc, stride)
+
+
+def merge_partials(partial: torch.Tensor, m: int, group=None, all_gather: bool = True,
+                   merge_fn: Callable | None = None) -> torch.Tensor:
+    """OR-merge every rank's full-size partial filter (int64 tensor of >= world*S
+    words, padding zero).  Returns the whole merged filter (all_gather=True) or this
+    rank's owned slice of S words."""
+    world = dist.get_world_size(group)
+    S = slice_words(m, world)
+    if partial.numel() < world * S:
+        raise ValueError("partial filter must be padded to world * slice_words(m) words")
+    send = partial[: world * S].contiguous()
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)          # recv[j*S:(j+1)*S] = slice of rank j
+    owned = torch.zeros(S, dtype=partial.dtype, device=partial.device)
+    (merge_fn or _hip_merge)(owned, recv, world, S)
+    if not all_gather:
+        return owned
+    full = torch.empty(world * S, dtype=partial.dtype, device=partial.device)
+    dist.all_gather_into_tensor(full, owned, group=group)
+    return full
+
+
+def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len: int, n: int,
+                      m: int, k: int, seed: int, flavor: int, group=None,
+                      all_gather: bool = True, build_fn: Callable | None = None,
+                      merge_fn: Callable | None = None, stream=None) -> torch.Tensor:
+    """Cooperative single-filter build.  `keys`/`offsets` hold THIS rank's key range
+    (offsets relative to `keys`, n+1 entries; or fixed key_len).  Every rank passes
+    the same (m, k, seed, flavor)."""
+    world = dist.get_world_size(group)
+    S = slice_words(m, world)
+    partial = torch.zeros(world * S, dtype=torch.int64, device=keys.device)
+    if build_fn is None:
+        build_device(keys, offsets, key_len, n, m, k, seed, flavor, partial, stream=stream,
+                     overwrite=True)
+    else:
+        build_fn(keys, offsets, key_len, n, m, k, seed, flavor, partial)
+    return merge_partials(partial, m, group=group, all_gather=all_gather, merge_fn=merge_fn)
+
+
+def build_independent(keys: torch.Tensor, offsets: torch.Tensor | None, key_len: int, n: int,
+                      m: int, k: int, seed: int, flavor: int, words: torch.Tensor,
+                      stream=None) -> None:
+    """One SSTable filter per rank: a plain device build, no collective."""
+    build_device(keys, offsets, key_len, n, m, k, seed, flavor, words, stream=stream,
+                 overwrite=True)

@@ -1,0 +1,155 @@
+// Drop-in class test: drives nasp-key-value-engine_amd/host/BloomFilter the way
+// the reference's callers do and checks every image bit for bit against the
+// oracle (oracle/bloom_oracle.c).  Needs a GPU (the class builds on the device).
+//   1. reference test program flow (BloomFilter/main.cpp:28-117): BF(20, 0.05),
+//      10 names added, membership of added / absent names, BF(10, 0.1) round trip;
+//   2. SSTable::build usage (SSTable/SSTable.cpp:28-35): BF(records.size(), 0.01),
+//      add() per record key, copy-assign into a member, serialize();
+//   3. TypesManager usage (System/TypesManager.cpp:74-107): deserialize, add,
+//      serialize (accumulate), then probe;
+//   4. the reference's committed MSVC filters with the FNV flavour.
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/nasp_bloom.h"
+#include "../../nasp-key-value-engine_amd/host/BloomFilter.h"
+extern "C" {
+#include "../../oracle/bloom_oracle.h"
+}
+
+static int failures = 0;
+#define EXPECT(cond, msg)                                     \
+    do {                                                      \
+        if (!(cond)) {                                        \
+            std::printf("FAIL: %s (line %d)\n", msg, __LINE__); \
+            ++failures;                                       \
+        }                                                     \
+    } while (0)
+
+static std::vector<uint8_t> oracle_image(const std::vector<std::string> &keys, uint32_t m,
+                                         uint32_t k, double p, uint32_t tc, uint64_t seed,
+                                         int flavor, const std::vector<uint64_t> *start = nullptr) {
+    std::vector<uint8_t> buf;
+    std::vector<uint64_t> offs{0};
+    for (auto &s : keys) {
+        buf.insert(buf.end(), s.begin(), s.end());
+        offs.push_back(buf.size());
+    }
+    buf.resize(buf.size() + 16);
+    std::vector<uint64_t> words = start ? *start : std::vector<uint64_t>((m + 63) / 64 + 1, 0);
+    orc_build(flavor, buf.data(), offs.data(), 0, keys.size(), m, k, seed, words.data());
+    std::vector<uint8_t> img(orc_serialized_size(m));
+    orc_serialize(m, k, p, tc, seed, words.data(), img.data());
+    return img;
+}
+
+static std::vector<uint8_t> bytes_of(const std::vector<std::byte> &v) {
+    return std::vector<uint8_t>(reinterpret_cast<const uint8_t *>(v.data()),
+                                reinterpret_cast<const uint8_t *>(v.data()) + v.size());
+}
+
+static void header(const std::vector<uint8_t> &img, uint32_t *m, uint32_t *k, double *p,
+                   uint32_t *tc, uint64_t *seed) {
+    std::memcpy(m, img.data(), 4);
+    std::memcpy(k, img.data() + 4, 4);
+    std::memcpy(p, img.data() + 8, 8);
+    std::memcpy(tc, img.data() + 16, 4);
+    std::memcpy(seed, img.data() + 20, 8);
+}
+
+int main() {
+    if (nb_device_count() < 1) {
+        std::printf("SKIP: no GPU\n");
+        return 77;
+    }
+    // 1. reference test program flow
+    {
+        BloomFilter bf(20, 0.05);
+        std::vector<std::string> added = {"Ana", "Marko", "Jelena", "Nikola", "Maja",
+                                          "Stefan", "Marina", "Petar", "Ivana", "Luka"};
+        for (auto &e : added) bf.add(e);
+        for (auto &e : added) EXPECT(bf.possiblyContains(e), "added name must be present");
+        auto img = bytes_of(bf.serialize());
+        uint32_t m, k, tc; double p; uint64_t seed;
+        header(img, &m, &k, &p, &tc, &seed);
+        EXPECT(m == orc_size_of_bitset(20, 0.05) && k == orc_num_hashes(20, m), "m/k formulas");
+        EXPECT(seed == orc_seed_from_time(tc), "seed from timeConst");
+        EXPECT(img == oracle_image(added, m, k, p, tc, seed, 0), "BF(20,0.05) image");
+        // absent names: same answers as the oracle's probe
+        std::vector<std::string> absent = {"Anja", "Marija", "Jovan", "Nina", "Milan", "Stefania",
+                                           "Marin", "Pera", "Iva", "Lukas", "Bogdan", "Elena"};
+        std::vector<uint64_t> words((m + 63) / 64 + 1, 0);
+        std::memcpy(words.data(), img.data() + 28, img.size() - 28);
+        for (auto &e : absent) {
+            uint8_t o = 0;
+            orc_probe(0, reinterpret_cast<const uint8_t *>(e.data()), nullptr, (uint32_t)e.size(), 1,
+                      m, k, seed, words.data(), &o);
+            EXPECT(bf.possiblyContains(e) == (o != 0), "absent-name answer matches oracle");
+        }
+        BloomFilter original(10, 0.1);
+        for (const char *e : {"Jedan", "Dva", "Tri"}) original.add(e);
+        BloomFilter restored = BloomFilter::deserialize(original.serialize());
+        for (const char *e : {"Jedan", "Dva", "Tri", "Cetiri"})
+            EXPECT(original.possiblyContains(e) == restored.possiblyContains(e), "round trip");
+        EXPECT(bytes_of(original.serialize()) == bytes_of(restored.serialize()), "round trip image");
+    }
+    // 2. SSTable::build usage: 50k sorted records, copy-assign, serialize
+    {
+        std::vector<std::string> recs;
+        for (int i = 0; i < 50000; ++i) {
+            char b[32];
+            std::snprintf(b, sizeof b, "user%012d", i);
+            recs.push_back(b);
+        }
+        BloomFilter member;
+        BloomFilter bf(recs.size(), 0.01);
+        for (auto &r : recs) bf.add(r);
+        member = bf;  // bloom_ = bf (SSTable.cpp:35)
+        auto img = bytes_of(member.serialize());
+        uint32_t m, k, tc; double p; uint64_t seed;
+        header(img, &m, &k, &p, &tc, &seed);
+        EXPECT(img == oracle_image(recs, m, k, p, tc, seed, 0), "SSTable-style build image");
+        int present = 0;
+        for (auto &r : recs) present += member.possiblyContains(r);
+        EXPECT(present == (int)recs.size(), "no false negatives");
+    }
+    // 3. TypesManager usage: deserialize -> add -> serialize accumulates
+    {
+        BloomFilter bf(1000, 0.01);
+        bf.add("alpha");
+        auto first = bf.serialize();
+        BloomFilter again = BloomFilter::deserialize(first);
+        again.add("beta");
+        again.add(std::string("\0gamma", 6));
+        auto img = bytes_of(again.serialize());
+        uint32_t m, k, tc; double p; uint64_t seed;
+        header(img, &m, &k, &p, &tc, &seed);
+        EXPECT(img == oracle_image({"alpha", "beta", std::string("\0gamma", 6)}, m, k, p, tc, seed, 0),
+               "accumulate after deserialize");
+        EXPECT(again.possiblyContains("alpha") && again.possiblyContains("beta"), "accumulated keys");
+        BloomFilter def;
+        EXPECT(def.possiblyContains("anything"), "default filter answers true");
+    }
+    // 4. an MSVC-written filter (level_0/filter_0.sst payload) with the FNV flavour
+    {
+        const uint8_t img0[31] = {0x14, 0, 0, 0, 7, 0, 0, 0, 0x7b, 0x14, 0xae, 0x47, 0xe1, 0x7a,
+                                  0x84, 0x3f, 0xb7, 0x0f, 0x3f, 0x68, 0xb7, 0x1c, 0x25, 0x6e,
+                                  0x0b, 0xde, 0x4d, 0xec, 0x2a, 0x2a, 0x0a};
+        std::vector<std::byte> v(31);
+        std::memcpy(v.data(), img0, 31);
+        BloomFilter::setDefaultFlavor(NB_FLAVOR_MSVC_FNV1A);
+        BloomFilter f = BloomFilter::deserialize(v);
+        EXPECT(f.possiblyContains("test") && f.possiblyContains("test2"), "MSVC filter members");
+        BloomFilter rebuilt = BloomFilter::deserialize(v);
+        rebuilt.add("test");
+        rebuilt.add("test2");
+        EXPECT(bytes_of(rebuilt.serialize()) == std::vector<uint8_t>(img0, img0 + 31),
+               "re-adding the members leaves the MSVC image unchanged");
+        BloomFilter::setDefaultFlavor(NB_FLAVOR_LIBSTDCXX);
+    }
+    nb_shutdown();
+    std::printf(failures ? "FAILED %d\n" : "drop-in OK\n", failures);
+    return failures ? 1 : 0;
+}

@@ -401,3 +401,43 @@ def test_bloomfilter_class_mirror(dev, oracle, golden):
     assert bf2.possiblyContains("Bogdan") and all(bf2.possiblyContains(e) for e in added)
     # default filter: everything "possibly" present
     assert nbm.BloomFilter().possiblyContains("x")
+
+
+# ------------------------------------------------------------ multi-GPU --
+
+def test_or_merge_kernel(dev):
+    import torch
+    import nasp_bloom as nbm
+    g = torch.Generator(device="cpu").manual_seed(5)
+    for nsrc, nw in ((1, 1), (3, 1000), (8, 65_537)):
+        src = torch.randint(-2**62, 2**62, (nsrc, nw + 3), generator=g, dtype=torch.int64)
+        dst = torch.randint(-2**62, 2**62, (nw,), generator=g, dtype=torch.int64)
+        want = dst.clone()
+        for s in range(nsrc):
+            want |= src[s, :nw]
+        d_dst, d_src = dst.to(dev), src.to(dev)
+        nbm.or_merge_device(d_dst, d_src, nw, nsrc, nw + 3)
+        torch.cuda.synchronize()
+        assert torch.equal(d_dst.cpu(), want)
+
+
+def test_cooperative_build_single_rank(dev, oracle):
+    """The cooperative (C5) path end to end on one GPU through RCCL (world size 1):
+    partial build + all-to-all + HIP OR-merge + all-gather."""
+    import os
+    import torch
+    import torch.distributed as dist
+    from nasp_bloom import distributed as D
+    from nasp_bloom import synth
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    n = 1_000_000
+    buf = synth.fixed_keys(n, 32)
+    full = D.build_cooperative(t_u8(buf, dev), None, 32, n, synth.C5.m, synth.C5.k, SEED, 0)
+    torch.cuda.synchronize()
+    want = oracle.build(0, buf, None, 32, n, synth.C5.m, synth.C5.k, SEED)
+    got = full.cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(got[: want.size], want)
+    dist.destroy_process_group()
