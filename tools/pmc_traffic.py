@@ -27,6 +27,13 @@ def per_kernel(path, counter):
     return {k: sum(v) / len(v) for k, v in acc.items()}
 
 
+def short(name):
+    """'void (anonymous namespace)::bloom_bin_kernel<0, 2, ...>(args)' -> 'bloom_bin_kernel<0, 2, ...>'"""
+    import re
+    m = re.search(r"([A-Za-z_][A-Za-z_0-9]*(<[^()]*>)?)\(", name)
+    return m.group(1) if m else name
+
+
 def kernel_sha():
     h = hashlib.sha256()
     for f in ("csrc/bloom_kernels.hip", "csrc/bloom_math.h"):
@@ -41,19 +48,21 @@ def main(tag, wl_key, prof_dir):
     fetch = per_kernel(os.path.join(prof_dir, "fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(prof_dir, "write", "run_counter_collection.csv"), "WRITE_SIZE")
     parts = {}
-    total = 0.0
     for name in fetch:
         if "bloom_bin_kernel" in name or "bloom_tile_or_kernel" in name:
             f, w = fetch[name], write.get(name, 0.0)
-            b = (2 * f + w) * 1024
-            parts[name.split("(")[0]] = {"FETCH_SIZE_KB": round(f, 1), "WRITE_SIZE_KB": round(w, 1),
-                                         "hbm_bytes": int(b)}
-            total += b
+            parts[short(name)] = {"FETCH_SIZE_KB": round(f, 1), "WRITE_SIZE_KB": round(w, 1),
+                                  "hbm_bytes": int((2 * f + w) * 1024)}
+    # one bench build = the bin kernel + the overwrite-mode tile kernel
+    # (OR-mode tile calls in the profile come from bench's host-path leg)
+    used = [k for k in parts if "bloom_bin_kernel" in k or ("tile_or" in k and "true" in k)]
+    total = sum(parts[k]["hbm_bytes"] for k in used)
     stats = {}
     for r in csv.DictReader(open(os.path.join(prof_dir, "trace", "run_kernel_stats.csv"))):
-        stats[r["Name"].split("(")[0]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
+        stats[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
     out = {"workload": wl.name, "kernel_source_sha": kernel_sha(),
-           "hbm_bytes_per_launch": int(total), "per_kernel": parts, "kernel_stats": stats,
+           "hbm_bytes_per_launch": int(total), "build_kernels": used, "per_kernel": parts,
+           "kernel_stats": stats,
            "source": f"profiles/{tag}_pmc_{wl_key}.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE "
                      "separate passes, FETCH_SIZE x2 gfx950 correction)"}
     dst = os.path.join(REPO, "profiles", f"{tag}_pmc_{wl_key}.json")
