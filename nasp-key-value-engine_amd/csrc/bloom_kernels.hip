@@ -94,6 +94,13 @@ struct KeyBatch {
             }
         }
     }
+    __device__ __forceinline__ void load_one(int p, const uint8_t *keys, const uint64_t *offsets,
+                                             uint64_t i, uint64_t n) {
+        if (i < n) {
+            if (LAYOUT == kFixed16) kv[p] = reinterpret_cast<const ulonglong2 *>(keys)[i];
+            else if (LAYOUT == kOffsets) { b[p] = offsets[i]; e[p] = offsets[i + 1]; }
+        }
+    }
     __device__ __forceinline__ void hash(const FilterConsts &c, const uint8_t *keys,
                                          uint32_t key_len, uint64_t i, int p, uint64_t *h1,
                                          uint64_t *h2) const {
@@ -360,25 +367,44 @@ __global__ __launch_bounds__(NT) void bloom_bin_kernel(
     if (NB_DIAG_STOP(1)) return;
 
     // phase 2: block-local run starts; reserve a run in every touched tile's
-    // bucket shard (cursor shard = blockIdx % G, laid out [shard][tile])
+    // bucket shard (cursor shard = blockIdx % G, laid out [shard][tile]).  Per tile
+    // the write-out needs only two words afterwards: G[t] := global entry index of
+    // the block's run minus S[t] (u32 wrap-around arithmetic), S[t] := first local
+    // position past the bucket's capacity.
     const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
     const uint32_t shard = blockIdx.x % tc.G;
     uint32_t *cur = sc.gcur + (size_t)shard * T;
     for (uint32_t t = tid; t < T; t += NT) {
-        const uint32_t h = cnt[t];
-        G[t] = h ? atomicAdd(&cur[t], h) : 0u;
-        cnt[t] = S[t];  // becomes the placement cursor
+        const uint32_t h = cnt[t], st = S[t];
+        const uint32_t g = h ? atomicAdd(&cur[t], h) : 0u;
+        cnt[t] = st;  // becomes the placement cursor
+        G[t] = (t * tc.G + shard) * tc.cap + g - st;
+        S[t] = st + (g < tc.cap ? tc.cap - g : 0u);
     }
     __syncthreads();
     if (NB_DIAG_STOP(2)) return;
 
-    // phase 3: regenerate the indices and counting-sort them by tile
+    // phase 3: regenerate the indices and counting-sort them by tile (all k
+    // cursor atomics of a key issued before their results are consumed)
 #pragma unroll
     for (int p = 0; p < KPT; ++p) {
         const uint64_t i = base + (uint64_t)p * NT + tid;
         if (i < n) {
             IndexGen g = gen[p];
-            for (uint32_t j = 0; j < c.k; ++j) {
+            uint32_t j = 0;
+            for (; j + 4 <= c.k; j += 4) {
+                uint32_t r[4], q[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (j + u) g.next(c);
+                    r[u] = g.r;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) q[u] = atomicAdd(&cnt[r[u] >> tc.ts], 1u);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) sorted[q[u]] = r[u];
+            }
+            for (; j < c.k; ++j) {
                 if (j) g.next(c);
                 sorted[atomicAdd(&cnt[g.r >> tc.ts], 1u)] = g.r;
             }
@@ -387,20 +413,34 @@ __global__ __launch_bounds__(NT) void bloom_bin_kernel(
     __syncthreads();
     if (NB_DIAG_STOP(3)) return;
 
-    // phase 4: coalesced write-out of the runs (spill beyond capacity)
+    // phase 4: coalesced write-out of the runs (spill beyond capacity), four
+    // independent entries per lane per step so the LDS lookups overlap
     const uint32_t tmask = (1u << tc.ts) - 1;
-    for (uint32_t j = tid; j < total; j += NT) {
-        const uint32_t v = sorted[j];
-        const uint32_t t = v >> tc.ts;
-        const uint32_t pos = G[t] + (j - S[t]);
-        if (pos < tc.cap) {
-            buckets[((size_t)t * tc.G + shard) * tc.cap + pos] =
-                (ENTRY)(sizeof(ENTRY) == 2 ? (v & tmask) : v);
+    auto emit = [&](uint32_t j, uint32_t v, uint32_t gb, uint32_t lim) {
+        if (j < lim) {
+            buckets[gb + j] = (ENTRY)(sizeof(ENTRY) == 2 ? (v & tmask) : v);
         } else {
             __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
-            sc.spill_flag[t] = 1u;
+            sc.spill_flag[v >> tc.ts] = 1u;
         }
+    };
+    uint32_t j = tid;
+    for (; j + 3 * NT < total; j += 4 * NT) {
+        uint32_t v[4], gb[4], lim[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            gb[u] = G[v[u] >> tc.ts];
+            lim[u] = S[v[u] >> tc.ts];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) emit(j + u * NT, v[u], gb[u], lim[u]);
+    }
+    for (; j < total; j += NT) {
+        const uint32_t v = sorted[j];
+        emit(j, v, G[v >> tc.ts], S[v >> tc.ts]);
     }
 }
 
@@ -695,6 +735,14 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         NB_HIP(hipGetLastError());
     }
     return NB_OK;
+}
+
+int num_cus() {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+        return 256;
+    return n;
 }
 
 template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE>

@@ -50,12 +50,14 @@ static void set_stagger(int blocks, int cycles) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_stagger_cycles), &cycles, sizeof cycles));
 }
 
+static size_t g_lds_pad = 0;  // extra dynamic LDS (forces fewer blocks per CU)
+
 template <int KPT, typename E>
 static float time_bin(const uint8_t *keys, uint64_t n, const FilterConsts &c, TileCfg tc,
                       TileScratch sc, void *buckets, int stop) {
     constexpr int NT = kBinThreads;
     constexpr uint64_t kpb = (uint64_t)KPT * NT;
-    const size_t lds = (3ull * tc.T + 32 + kpb * c.k) * 4;
+    const size_t lds = (size_t)bin_sort_offset_words(tc.T) * 4 + kpb * c.k * 4 + g_lds_pad;
     auto kern = bloom_bin_kernel<0, kFixed16, KPT, E>;
     if (lds > 160 * 1024) return -1.f;
     allow_lds(kern, lds);
@@ -127,15 +129,16 @@ int main() {
         tc.G = 8;
         double e = (double)n * k / ((double)tc.T * tc.G);
         tc.cap = ((uint32_t)(e + 8 * std::sqrt(e) + 64) + 7) & ~7u;
-        printf("ts=16 T=%u G=8 stagger sweep (full bin kernel, u16)\n", tc.T);
-        for (int sb : {0, 256, 128, 512})
-            for (int cyc : {2000, 8000, 20000, 40000}) {
-                set_stagger(sb, cyc);
-                printf("  stagger blocks [%d,%d) cycles %6d : %.4f ms\n", sb, 2 * sb, cyc,
-                       time_bin<kBinKPT, uint16_t>(keys, n, c, tc, sc, buckets, 0));
-                if (!sb) break;
-            }
-        set_stagger(0, 0);
+        for (size_t pad : {(size_t)0, (size_t)70 * 1024}) {
+            g_lds_pad = pad;
+            printf("ts=16 T=%u G=8 u16 lds_pad=%zu (%s block/CU): p1 %.4f p12 %.4f p123 %.4f full %.4f ms\n",
+                   tc.T, pad, pad ? "1" : "2",
+                   time_bin<kBinKPT, uint16_t>(keys, n, c, tc, sc, buckets, 1),
+                   time_bin<kBinKPT, uint16_t>(keys, n, c, tc, sc, buckets, 2),
+                   time_bin<kBinKPT, uint16_t>(keys, n, c, tc, sc, buckets, 3),
+                   time_bin<kBinKPT, uint16_t>(keys, n, c, tc, sc, buckets, 0));
+        }
+        g_lds_pad = 0;
     }
     CK(hipDeviceSynchronize());
     return 0;
