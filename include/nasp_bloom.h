@@ -130,6 +130,28 @@ size_t nb_serialize(uint32_t m, uint32_t k, double p, uint32_t time_const, uint6
 int nb_deserialize(const uint8_t *img, size_t len, uint32_t *m, uint32_t *k, double *p,
                    uint32_t *time_const, uint64_t *h2_seed, uint64_t *words);
 
+/* -------------------------------------------- SSTable filter write-back --- */
+/* The filter region of an SSTable exactly as the reference writes it:
+ *   NB_FRAME_RAW : u64 LE image length + image  (SSTableRaw::writeBloomToFile,
+ *                  SSTable/SSTableRaw.cpp:534-567)
+ *   NB_FRAME_COMP: LEB128 varint image length + image  (SSTableComp::writeBloomToFile,
+ *                  SSTable/SSTableComp.cpp:469-504, Utils/VarEncoding.h:13-27)
+ * cut into block_size blocks, the last one padded with '0' (0x30) bytes
+ * (Block_manager::write_block / fill_in_padding, block-manager/block-manager.cpp:12-44),
+ * so one write of nb_framed_filter_size() bytes at the region's block offset
+ * reproduces the file.  The image is nb_serialize()'s. */
+enum nb_framing { NB_FRAME_RAW = 0, NB_FRAME_COMP = 1 };
+size_t nb_framed_filter_size(uint32_t m, int framing, uint32_t block_size);
+size_t nb_frame_filter(uint32_t m, uint32_t k, double p, uint32_t time_const, uint64_t h2_seed,
+                       const uint64_t *words, int framing, uint32_t block_size, uint8_t *out);
+/* Same, with the filter words still in device memory: the header is written on
+ * the host and the bit payload is copied D2H straight into its place in `out`
+ * (host memory; pinned memory makes the copy asynchronous-capable).  Synchronises
+ * `stream` before returning. */
+int nb_frame_filter_device(uint32_t m, uint32_t k, double p, uint32_t time_const,
+                           uint64_t h2_seed, const uint64_t *d_words, int framing,
+                           uint32_t block_size, uint8_t *out, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

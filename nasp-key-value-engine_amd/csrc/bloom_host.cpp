@@ -58,4 +58,56 @@ int nb_deserialize(const uint8_t *img, size_t len, uint32_t *m, uint32_t *k, dou
     return NB_OK;
 }
 
+static size_t varint_len(uint64_t v) {
+    size_t n = 1;
+    while (v >>= 7) ++n;
+    return n;
+}
+
+static size_t frame_prefix(uint64_t img_len, int framing, uint8_t *out) {
+    if (framing == NB_FRAME_RAW) {
+        if (out) std::memcpy(out, &img_len, 8);
+        return 8;
+    }
+    size_t n = 0;
+    do {
+        uint8_t chunk = img_len & 0x7F;
+        img_len >>= 7;
+        if (img_len) chunk |= 0x80;
+        if (out) out[n] = chunk;
+        ++n;
+    } while (img_len);
+    return n;
+}
+
+size_t nb_framed_filter_size(uint32_t m, int framing, uint32_t block_size) {
+    const size_t img = nb_serialized_size(m);
+    const size_t payload = (framing == NB_FRAME_RAW ? 8 : varint_len(img)) + img;
+    if (block_size == 0) return payload;
+    return (payload + block_size - 1) / block_size * block_size;
+}
+
+size_t nb_frame_filter(uint32_t m, uint32_t k, double p, uint32_t time_const, uint64_t h2_seed,
+                       const uint64_t *words, int framing, uint32_t block_size, uint8_t *out) {
+    const size_t img = nb_serialized_size(m);
+    const size_t pre = frame_prefix(img, framing, out);
+    nb_serialize(m, k, p, time_const, h2_seed, words, out + pre);
+    const size_t total = nb_framed_filter_size(m, framing, block_size);
+    std::memset(out + pre + img, '0', total - pre - img);
+    return total;
+}
+
 }  // extern "C"
+
+// Host-side framing helpers shared with the device variant (bloom_kernels.hip).
+size_t nb_internal_frame_header(uint32_t m, uint32_t k, double p, uint32_t time_const,
+                                uint64_t h2_seed, int framing, uint8_t *out) {
+    const size_t img = nb_serialized_size(m);
+    const size_t pre = frame_prefix(img, framing, out);
+    std::memcpy(out + pre + 0, &m, 4);
+    std::memcpy(out + pre + 4, &k, 4);
+    std::memcpy(out + pre + 8, &p, 8);
+    std::memcpy(out + pre + 16, &time_const, 4);
+    std::memcpy(out + pre + 20, &h2_seed, 8);
+    return pre + 28;  // offset of the bit payload
+}

@@ -30,6 +30,9 @@
 
 using nb::FilterConsts;
 
+size_t nb_internal_frame_header(uint32_t m, uint32_t k, double p, uint32_t time_const,
+                                uint64_t h2_seed, int framing, uint8_t *out);  // bloom_host.cpp
+
 namespace {
 
 enum Layout : int { kOffsets = 0, kFixedStride = 1, kFixed16 = 2 };
@@ -1039,6 +1042,21 @@ int nb_probe_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t k
     if (rc) return rc;
     return launch_probe(d_keys, d_offsets, key_len, n, m, k, h2_seed, flavor, d_words, d_out,
                         (hipStream_t)stream);
+}
+
+int nb_frame_filter_device(uint32_t m, uint32_t k, double p, uint32_t time_const,
+                           uint64_t h2_seed, const uint64_t *d_words, int framing,
+                           uint32_t block_size, uint8_t *out, void *stream) {
+    if (!out || (m && !d_words)) return fail(NB_ERR_ARG, "NULL buffer");
+    if (framing != NB_FRAME_RAW && framing != NB_FRAME_COMP) return fail(NB_ERR_ARG, "framing");
+    const size_t body = nb_internal_frame_header(m, k, p, time_const, h2_seed, framing, out);
+    const size_t nbytes = (uint32_t)(m + 7u) / 8u;  // the reference's 32-bit (m+7)/8
+    hipStream_t st = (hipStream_t)stream;
+    if (nbytes) NB_HIP(hipMemcpyAsync(out + body, d_words, nbytes, hipMemcpyDeviceToHost, st));
+    const size_t total = nb_framed_filter_size(m, framing, block_size);
+    std::memset(out + body + nbytes, '0', total - body - nbytes);
+    NB_HIP(hipStreamSynchronize(st));
+    return NB_OK;
 }
 
 int nb_or_merge_device(uint64_t *d_dst, const uint64_t *d_src, uint64_t nwords, uint32_t nsrc,

@@ -23,8 +23,16 @@
 // A failed device build throws std::runtime_error: there is no CPU fallback.
 #pragma once
 
+// The reference header's includes are kept: its callers rely on them
+// transitively (e.g. SSTable.cpp uses std::memcpy via <cstring>).
+#include <cmath>
 #include <cstddef>
 #include <cstdint>
+#include <cstring>
+#include <ctime>
+#include <functional>
+#include <random>
+#include <stdexcept>
 #include <string>
 #include <vector>
 

@@ -51,7 +51,16 @@ _SIGS = {
                                   C.c_void_p, C.c_void_p]),
     "nb_deserialize": (C.c_int, [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_void_p, C.c_void_p, C.c_void_p]),
+    "nb_framed_filter_size": (C.c_size_t, [C.c_uint32, C.c_int, C.c_uint32]),
+    "nb_frame_filter": (C.c_size_t, [C.c_uint32, C.c_uint32, C.c_double, C.c_uint32, C.c_uint64,
+                                     C.c_void_p, C.c_int, C.c_uint32, C.c_void_p]),
+    "nb_frame_filter_device": (C.c_int, [C.c_uint32, C.c_uint32, C.c_double, C.c_uint32,
+                                         C.c_uint64, C.c_void_p, C.c_int, C.c_uint32,
+                                         C.c_void_p, C.c_void_p]),
 }
+
+FRAME_RAW = 0
+FRAME_COMP = 1
 
 _LIB = None
 

@@ -1,0 +1,73 @@
+// ref_engine_harness.cpp -- drives the reference engine's SSTable writer and LSM
+// compaction (our code; the engine sources are compiled where they lie).
+//
+// Built twice (oracle/Makefile `ref-engine`, nasp-key-value-engine_amd/Makefile
+// `engine-dropin`):
+//   * against the reference BloomFilter.cpp  -> oracle/_ref/ref_engine
+//   * against the MI355X drop-in class       -> nasp-key-value-engine_amd/build/engine_dropin
+// Both write real SSTables through SSTManager::write (SSTable/SSTManager.cpp:274-359),
+// so the filter files on disk come from SSTable::build (SSTable/SSTable.cpp:28-35)
+// and writeBloomToFile (SSTableRaw.cpp:534-567 / SSTableComp.cpp:469-504).
+// tests/test_engine_dropin.py checks every filter file against the oracle and the
+// drop-in run against the reference run.
+//
+// usage: engine <data_dir> <raw|comp> <n_records> <block_size> [tiered]
+//   writes one level-1 SSTable of n records ("user%012d" keys); with `tiered`,
+//   writes three tables and runs LSMManager::triggerCompactionCheck
+//   (size-tiered, LSM/LSMManager.cpp:203-233) so a level-2 table is compacted.
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "Config.h"
+#include "LSMManager.h"
+#include "SSTManager.h"
+#include "block-manager.h"
+
+static std::vector<Record> records(int first, int n) {
+    std::vector<Record> out;
+    out.reserve(n);
+    for (int i = 0; i < n; ++i) {
+        char k[32], v[32];
+        std::snprintf(k, sizeof k, "user%012d", first + i);
+        std::snprintf(v, sizeof v, "value-%d", first + i);
+        Record r{};
+        r.key = k;
+        r.value = v;
+        r.key_size = r.key.size();
+        r.value_size = r.value.size();
+        r.timestamp = 1000000ull + (unsigned long long)(first + i);
+        r.tombstone = std::byte{0};
+        out.push_back(r);
+    }
+    return out;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 5) {
+        std::fprintf(stderr, "usage: %s <dir> <raw|comp> <n> <block_size> [tiered]\n", argv[0]);
+        return 2;
+    }
+    Config::data_directory = argv[1];
+    Config::compress_sstable = std::strcmp(argv[2], "comp") == 0;
+    Config::sstable_single_file = false;
+    const int n = std::atoi(argv[3]);
+    Config::block_size = std::atoi(argv[4]);
+    const bool tiered = argc > 5 && std::strcmp(argv[5], "tiered") == 0;
+    Config::compaction_strategy = "tiered";
+    Config::max_levels = 4;
+    Config::max_number_of_sstable_on_level = 3;
+
+    Block_manager bm;
+    SSTManager sst(&bm);
+    if (!tiered) {
+        sst.write(records(0, n), 1);
+    } else {
+        for (int t = 0; t < 3; ++t) sst.write(records(t * (n / 2), n), 1);  // overlapping ranges
+        LSMManager lsm(&sst);
+        lsm.triggerCompactionCheck();
+    }
+    std::printf("engine done\n");
+    return 0;
+}

@@ -1,0 +1,149 @@
+"""The reference engine's own SSTable writer and size-tiered compaction, run twice:
+
+* `oracle/_ref/ref_engine`: the reference engine with the reference BloomFilter
+  (compiled in place by oracle/Makefile `ref-engine`) -- pins the on-disk filter
+  framing (u64 / varint length prefix, '0' block padding) that nb_frame_filter
+  must reproduce, on CPU;
+* `nasp-key-value-engine_amd/build/engine_dropin`: the same engine sources linked
+  against the MI355X drop-in class (Makefile `engine-dropin`) -- on the GPU, every
+  filter file it writes through SSTable::build / writeBloomToFile must be
+  bit-exact (oracle) and byte-identical in framing to what the reference writes.
+
+Both binaries are built in the build container (they need /root/reference) and
+travel to the GPU box as built artifacts."""
+import os
+import re
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ORACLE, PKG
+
+REF_ENGINE = os.path.join(ORACLE, "_ref", "ref_engine")
+DROPIN_ENGINE = os.path.join(PKG, "build", "engine_dropin")
+
+
+def keys_for(n_tables, n):
+    """Keys the harness writes (oracle/ref_engine_harness.cpp `records`)."""
+    if n_tables == 1:
+        idx = range(n)
+    else:  # three overlapping tables t*(n/2) .. t*(n/2)+n, merged and deduplicated
+        idx = sorted({t * (n // 2) + i for t in range(3) for i in range(n)})
+    return [b"user%012d" % i for i in idx]
+
+
+def run_engine(exe, d, mode, n, bs, tiered=False):
+    args = [exe, str(d), mode, str(n), str(bs)] + (["tiered"] if tiered else [])
+    out = subprocess.run(args, capture_output=True, timeout=600)  # the engine prints raw bytes
+    if out.returncode != 0:
+        err = out.stderr[-2000:].decode(errors="replace")
+        raise AssertionError(f"{exe} failed rc={out.returncode}: {err}")
+
+
+def filter_files(d):
+    found = []
+    for root, _, files in os.walk(d):
+        for f in files:
+            if re.match(r"filter_(raw|comp)_\d+\.db$", f):
+                found.append(os.path.join(root, f))
+    return sorted(found)
+
+
+def parse_framed(raw, comp):
+    if not comp:
+        (length,) = struct.unpack("<Q", raw[:8])
+        pre = 8
+    else:
+        length, shift, pre = 0, 0, 0
+        while True:
+            b = raw[pre]
+            length |= (b & 0x7F) << shift
+            shift += 7
+            pre += 1
+            if not b & 0x80:
+                break
+    return raw[pre:pre + length]
+
+
+def check_filter_file(path, keys, bs, oracle, nbm):
+    raw = open(path, "rb").read()
+    comp = "_comp_" in os.path.basename(path)
+    img = parse_framed(raw, comp)
+    m, k, p, tc, seed, words = nbm.deserialize(img)
+    assert seed == oracle.seed_from_time(tc)
+    # bit-exact against the oracle on the table's keys (libstdc++ flavour)
+    buf = np.frombuffer(b"".join(keys) + b"\0" * 16, np.uint8).copy()
+    offs = np.zeros(len(keys) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in keys])
+    want = oracle.serialize(m, k, p, tc, seed, oracle.build(0, buf, offs, 0, len(keys), m, k, seed))
+    assert img == want, path
+    # the framing nb_frame_filter produces is the file, byte for byte
+    h = nbm.lib()
+    size = h.nb_framed_filter_size(m, 1 if comp else 0, bs)
+    out = np.zeros(size, np.uint8)
+    n = h.nb_frame_filter(m, k, p, tc, seed, words.ctypes.data, 1 if comp else 0, bs, out.ctypes.data)
+    assert n == size == len(raw)
+    assert out.tobytes() == raw, path
+    return m, k
+
+
+@pytest.mark.parametrize("mode", ["raw", "comp"])
+@pytest.mark.parametrize("bs", [4096, 75])
+def test_reference_engine_framing(tmp_path, oracle, mode, bs, built):
+    """nb_frame_filter reproduces the reference engine's filter files exactly."""
+    if not os.path.exists(REF_ENGINE):
+        pytest.skip("oracle/_ref/ref_engine not built (needs /root/reference)")
+    import nasp_bloom as nbm
+    run_engine(REF_ENGINE, tmp_path, mode, 1000, bs)
+    files = filter_files(tmp_path)
+    assert len(files) == 1
+    m, k = check_filter_file(files[0], keys_for(1, 1000), bs, oracle, nbm)
+    assert (m, k) == (9586, 7)
+
+
+@pytest.mark.parametrize("mode", ["raw", "comp"])
+def test_reference_engine_tiered_compaction(tmp_path, oracle, mode, built):
+    """The reference engine's size-tiered compaction output filter (k-way merged,
+    deduplicated keys) is what the oracle and nb_frame_filter predict."""
+    if not os.path.exists(REF_ENGINE):
+        pytest.skip("oracle/_ref/ref_engine not built (needs /root/reference)")
+    import nasp_bloom as nbm
+    run_engine(REF_ENGINE, tmp_path, mode, 3000, 4096, tiered=True)
+    lvl2 = [f for f in filter_files(tmp_path) if "/level_2/" in f]
+    assert len(lvl2) == 1
+    check_filter_file(lvl2[0], keys_for(3, 3000), 4096, oracle, nbm)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["raw", "comp"])
+@pytest.mark.parametrize("tiered", [False, True])
+def test_engine_with_dropin_on_gpu(tmp_path, oracle, mode, tiered, built):
+    """The reference engine linked against the drop-in class: flush and size-tiered
+    compaction write filters bit-exact with the oracle, framed exactly as the
+    reference frames them, and with the same file set as the reference engine."""
+    if not os.path.exists(DROPIN_ENGINE):
+        pytest.skip("engine_dropin not built (needs /root/reference at build time)")
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import nasp_bloom as nbm
+    n, bs = 3000, 4096
+    d_new = tmp_path / "dropin"
+    run_engine(DROPIN_ENGINE, d_new, mode, n, bs, tiered)
+    files = filter_files(d_new)
+    if tiered:
+        lvl2 = [f for f in files if "/level_2/" in f]
+        assert len(lvl2) == 1, files
+        check_filter_file(lvl2[0], keys_for(3, n), bs, oracle, nbm)
+    else:
+        assert len(files) == 1
+        check_filter_file(files[0], keys_for(1, n), bs, oracle, nbm)
+    if os.path.exists(REF_ENGINE):
+        d_ref = tmp_path / "ref"
+        run_engine(REF_ENGINE, d_ref, mode, n, bs, tiered)
+        rel = lambda fs, d: sorted(os.path.relpath(f, d) for f in fs)
+        assert rel(filter_files(d_ref), d_ref) == rel(files, d_new)
+        for f in filter_files(d_ref):
+            assert os.path.getsize(f) == os.path.getsize(d_new / os.path.relpath(f, d_ref))
