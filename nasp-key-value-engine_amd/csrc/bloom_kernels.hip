@@ -259,11 +259,15 @@ __device__ uint32_t block_exclusive_scan(const uint32_t *hist, uint32_t *S, uint
     }
     __syncthreads();
     uint32_t run = wave_sums[wid] + incl - local;
+    const uint32_t total = wave_sums[kWaves];
     for (uint32_t t = b; t < e; ++t) {
         S[t] = run;
         run += hist[t];
     }
-    return wave_sums[kWaves];
+    // Threads own contiguous runs of tiles here but callers walk tiles strided by
+    // NT (and may overwrite hist): the barrier orders the two when T > NT.
+    __syncthreads();
+    return total;
 }
 
 // LDS carve of the bin kernel: cnt | S | G | wave_sums[32] | sort/stage area,
