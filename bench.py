@@ -157,15 +157,11 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     seed = synth.H2_SEED
 
-    def step(ev=None):
+    def step():
         with torch.cuda.stream(stream):
-            if ev is not None:
-                ev[0].record(stream)
             # a fresh filter per step (overwrite mode: no separate clear pass)
             nbm.build_device(keys, offs, key_len, wl.n, wl.m, wl.k, seed, args.flavor, words,
                              stream=stream, overwrite=True)
-            if ev is not None:
-                ev[1].record(stream)
 
     for _ in range(args.warmup):
         step()
@@ -178,19 +174,23 @@ def main():
         raise SystemExit("build produced a false negative -- refusing to report")
     del probe_out
 
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+    # HIP events on the build stream bracket the K builds (one pair: per-step
+    # event packets would put a ~10 us bubble between builds); kern_ms is the
+    # average device time of one build call
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(events[i])
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
 
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)

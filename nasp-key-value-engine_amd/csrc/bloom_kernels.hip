@@ -132,22 +132,7 @@ __device__ __forceinline__ void hashes_of(const FilterConsts &c, const uint8_t *
 
 // Index stream of one key: r_0 = h1 mod m, then r_{j+1} = r_j + (h2 mod m) with a
 // -(2^64 mod m) correction whenever the 64-bit x_j = h1 + j*h2 wraps.
-struct IndexGen {
-    uint64_t x, h2;
-    uint32_t r, s;
-    __device__ __forceinline__ void start(uint64_t h1_, uint64_t h2_, const FilterConsts &c) {
-        x = h1_;
-        h2 = h2_;
-        r = nb::mod64(h1_, c.fm);
-        s = nb::mod64(h2_, c.fm);
-    }
-    __device__ __forceinline__ void next(const FilterConsts &c) {
-        const uint64_t nx = x + h2;
-        r = nb::addmod(r, s, c.fm.m);
-        if (nx < x) r = nb::submod(r, c.c64, c.fm.m);
-        x = nx;
-    }
-};
+using nb::IndexGen;
 
 // Path A ("atomic"): one lane per key, k no-return agent-scope atomic ORs.
 // Bounded by the chip's atomic request rate (~27 G/s measured, tools/ubench.hip),
@@ -227,33 +212,41 @@ constexpr uint32_t kMaxTiles = 4096;
 #ifndef NB_DIAG_PROLOGUE
 #define NB_DIAG_PROLOGUE()
 #endif
+#ifndef NB_DIAG_NOCOUNT
+#define NB_DIAG_NOCOUNT false
+#endif
+
+// Inclusive prefix sum across a wave64 with DPP row shifts and the GFX9 row
+// broadcasts (6 VALU ops, no LDS round trips): Hillis-Steele inside each 16-lane
+// row, then row 15 -> rows 1,3 and lane 31 -> rows 2,3.  Lanes whose DPP source
+// is outside the row (or whose row is masked off) add `old` = 0.
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
 
 // Exclusive scan of hist[0..T) into S[0..T); returns the total.  blockDim = NT.
 template <int NT>
 __device__ uint32_t block_exclusive_scan(const uint32_t *hist, uint32_t *S, uint32_t T,
                                          uint32_t *wave_sums) {
     constexpr uint32_t kWaves = NT / 64;
+    static_assert(kWaves <= 64, "one wave scans the wave totals");
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t per = (T + NT - 1) / NT;
     const uint32_t b = min(tid * per, T), e = min(b + per, T);
     uint32_t local = 0;
     for (uint32_t t = b; t < e; ++t) local += hist[t];
-    uint32_t incl = local;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        uint32_t v = __shfl_up(incl, d, 64);
-        if (lane >= (uint32_t)d) incl += v;
-    }
+    const uint32_t incl = wave_inclusive_scan(local);
     if (lane == 63) wave_sums[wid] = incl;
     __syncthreads();
     if (wid == 0) {
-        uint32_t w = lane < kWaves ? wave_sums[lane] : 0;
-        uint32_t wi = w;
-#pragma unroll
-        for (int d = 1; d < (int)kWaves; d <<= 1) {
-            uint32_t v = __shfl_up(wi, d, 64);
-            if (lane >= (uint32_t)d) wi += v;
-        }
+        const uint32_t w = lane < kWaves ? wave_sums[lane] : 0;
+        const uint32_t wi = wave_inclusive_scan(w);
         if (lane < kWaves) wave_sums[lane] = wi - w;  // exclusive wave offsets
         if (lane == kWaves - 1) wave_sums[kWaves] = wi;  // total
     }
@@ -274,7 +267,7 @@ __device__ uint32_t block_exclusive_scan(const uint32_t *hist, uint32_t *S, uint
 // the last one 16-byte aligned (Guideline 17: misaligned b64/b128 LDS accesses
 // replay at 64 cycles per wave-instruction).
 __host__ __device__ constexpr uint32_t bin_sort_offset_words(uint32_t T) {
-    return (3 * T + 32 + 3) & ~3u;
+    return (2 * T + 32 + 3) & ~3u;
 }
 
 struct TileScratch {
@@ -284,32 +277,49 @@ struct TileScratch {
 };
 
 template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY, int NT = kBinThreads,
-          bool STAGE = (LAYOUT != kFixed16)>
+          bool STAGE = (LAYOUT != kFixed16), int KR = 0>
 __global__ __launch_bounds__(NT) void bloom_bin_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
     uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc, ENTRY *__restrict__ buckets) {
     extern __shared__ uint32_t lds[];
     const uint32_t T = tc.T;
-    uint32_t *cnt = lds;               // [T] per-tile counts, then placement cursors
+    uint32_t *cnt = lds;               // [T] per-tile counts (then placement cursors)
     uint32_t *S = cnt + T;             // [T] block-local run starts
-    uint32_t *G = S + T;               // [T] bucket positions of the runs
-    uint32_t *wave_sums = G + T;       // [NT/64 + 1]
+    uint2 *GL = reinterpret_cast<uint2 *>(lds);  // [T] over cnt|S once both are dead:
+                                       // {global entry index of the run - S[t], limit}
+    uint32_t *wave_sums = S + T;       // [NT/64 + 1]
     uint32_t *sorted = lds + bin_sort_offset_words(T);  // [KPB * k], 16-byte aligned
     const uint32_t tid = threadIdx.x;
     NB_DIAG_PROLOGUE();
     for (uint32_t t = tid; t < T; t += NT) cnt[t] = 0;
     __syncthreads();
 
-    // phase 1: hash each key once; count its k indices per tile.  Only the index
-    // generator's start state (6 registers per key) is kept for phase 3.
+    // phase 1: hash each key once; count its k indices per tile.  With KR > 0
+    // (k <= KR) the count atomic's return value is the index's rank in its tile's
+    // block-local run, and index + rank stay in registers for phase 3; otherwise
+    // only the index generator's start state (6 registers per key) is kept and
+    // phase 3 regenerates the indices.
+    constexpr int kR = KR > 0 ? KR : 1;
     IndexGen gen[KPT];
+    uint32_t ridx[KPT][kR], rank[KPT][kR];
     const uint64_t base = (uint64_t)blockIdx.x * (KPT * NT);
     auto count_key = [&](int p, uint64_t h1, uint64_t h2) {
         gen[p].start(h1, h2, c);
         IndexGen g = gen[p];
-        for (uint32_t j = 0; j < c.k; ++j) {
-            if (j) g.next(c);
-            atomicAdd(&cnt[g.r >> tc.ts], 1u);
+        if (KR > 0) {
+#pragma unroll
+            for (int j = 0; j < kR; ++j) {
+                if (j < (int)c.k) {
+                    if (j) g.next(c);
+                    ridx[p][j] = g.r;
+                    rank[p][j] = NB_DIAG_NOCOUNT ? g.r : atomicAdd(&cnt[g.r >> tc.ts], 1u);
+                }
+            }
+        } else {
+            for (uint32_t j = 0; j < c.k; ++j) {
+                if (j) g.next(c);
+                atomicAdd(&cnt[g.r >> tc.ts], 1u);
+            }
         }
     };
     if (!STAGE) {
@@ -381,51 +391,93 @@ __global__ __launch_bounds__(NT) void bloom_bin_kernel(
     const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
     const uint32_t shard = blockIdx.x % tc.G;
     uint32_t *cur = sc.gcur + (size_t)shard * T;
-    for (uint32_t t = tid; t < T; t += NT) {
-        const uint32_t h = cnt[t], st = S[t];
-        const uint32_t g = h ? atomicAdd(&cur[t], h) : 0u;
-        cnt[t] = st;  // becomes the placement cursor
-        G[t] = (t * tc.G + shard) * tc.cap + g - st;
-        S[t] = st + (g < tc.cap ? tc.cap - g : 0u);
+    // tiles owned by this thread in phase 2: t = tid + u*NT
+    constexpr int kTPT = (kMaxTiles + NT - 1) / NT;
+    uint32_t gres[kTPT], gl_g[kTPT], gl_l[kTPT];
+#pragma unroll
+    for (int u = 0; u < kTPT; ++u) {
+        const uint32_t t = tid + u * NT;
+        const uint32_t h = t < T ? cnt[t] : 0u;
+        gres[u] = h ? atomicAdd(&cur[t], h) : 0u;
     }
-    __syncthreads();
     if (NB_DIAG_STOP(2)) return;
-
-    // phase 3: regenerate the indices and counting-sort them by tile (all k
-    // cursor atomics of a key issued before their results are consumed)
+    // The {G, limit} pair of a tile: G = global entry index of the block's run
+    // minus its local start (u32 wrap-around), limit = first local position past
+    // the bucket's capacity.
+    auto run_pair = [&](int u, uint32_t t) {
+        const uint32_t st = S[t], g = gres[u];
+        gl_g[u] = (t * tc.G + shard) * tc.cap + g - st;
+        gl_l[u] = st + (g < tc.cap ? tc.cap - g : 0u);
+    };
+    if (KR > 0) {
+        // phase 3, rank mode: each index goes to its tile's run start + rank; the
+        // reservations' round trips overlap this LDS placement
 #pragma unroll
-    for (int p = 0; p < KPT; ++p) {
-        const uint64_t i = base + (uint64_t)p * NT + tid;
-        if (i < n) {
-            IndexGen g = gen[p];
-            uint32_t j = 0;
-            for (; j + 4 <= c.k; j += 4) {
-                uint32_t r[4], q[4];
+        for (int p = 0; p < KPT; ++p) {
+            const uint64_t i = base + (uint64_t)p * NT + tid;
+            if (i < n) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    if (j + u) g.next(c);
-                    r[u] = g.r;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) q[u] = atomicAdd(&cnt[r[u] >> tc.ts], 1u);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) sorted[q[u]] = r[u];
-            }
-            for (; j < c.k; ++j) {
-                if (j) g.next(c);
-                sorted[atomicAdd(&cnt[g.r >> tc.ts], 1u)] = g.r;
+                for (int j = 0; j < kR; ++j)
+                    if (j < (int)c.k) sorted[S[ridx[p][j] >> tc.ts] + rank[p][j]] = ridx[p][j];
             }
         }
+#pragma unroll
+        for (int u = 0; u < kTPT; ++u) {
+            const uint32_t t = tid + u * NT;
+            if (t < T) run_pair(u, t);
+        }
+    } else {
+        // phase 3, k > 16: regenerate the indices and counting-sort them with
+        // cursor atomics (all k of a key issued before their results are consumed)
+#pragma unroll
+        for (int u = 0; u < kTPT; ++u) {
+            const uint32_t t = tid + u * NT;
+            if (t < T) {
+                run_pair(u, t);
+                cnt[t] = S[t];  // placement cursor
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int p = 0; p < KPT; ++p) {
+            const uint64_t i = base + (uint64_t)p * NT + tid;
+            if (i < n) {
+                IndexGen g = gen[p];
+                uint32_t j = 0;
+                for (; j + 4 <= c.k; j += 4) {
+                    uint32_t r[4], q[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (j + u) g.next(c);
+                        r[u] = g.r;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) q[u] = atomicAdd(&cnt[r[u] >> tc.ts], 1u);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) sorted[q[u]] = r[u];
+                }
+                for (; j < c.k; ++j) {
+                    if (j) g.next(c);
+                    sorted[atomicAdd(&cnt[g.r >> tc.ts], 1u)] = g.r;
+                }
+            }
+        }
+    }
+    __syncthreads();  // cnt and S are dead: the pairs go over them
+#pragma unroll
+    for (int u = 0; u < kTPT; ++u) {
+        const uint32_t t = tid + u * NT;
+        if (t < T) GL[t] = make_uint2(gl_g[u], gl_l[u]);
     }
     __syncthreads();
     if (NB_DIAG_STOP(3)) return;
 
     // phase 4: coalesced write-out of the runs (spill beyond capacity), four
-    // independent entries per lane per step so the LDS lookups overlap
-    const uint32_t tmask = (1u << tc.ts) - 1;
-    auto emit = [&](uint32_t j, uint32_t v, uint32_t gb, uint32_t lim) {
-        if (j < lim) {
-            buckets[gb + j] = (ENTRY)(sizeof(ENTRY) == 2 ? (v & tmask) : v);
+    // independent entries per lane per step so the LDS lookups overlap.  Entries
+    // are stored unmasked (a u16 store keeps the low bits; the tile kernel masks).
+    auto emit = [&](uint32_t j, uint32_t v, uint2 gl) {
+        if (j < gl.y) {
+            buckets[gl.x + j] = (ENTRY)v;
         } else {
             __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
@@ -434,20 +486,18 @@ __global__ __launch_bounds__(NT) void bloom_bin_kernel(
     };
     uint32_t j = tid;
     for (; j + 3 * NT < total; j += 4 * NT) {
-        uint32_t v[4], gb[4], lim[4];
+        uint32_t v[4];
+        uint2 gl[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            gb[u] = G[v[u] >> tc.ts];
-            lim[u] = S[v[u] >> tc.ts];
-        }
+        for (int u = 0; u < 4; ++u) gl[u] = GL[v[u] >> tc.ts];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) emit(j + u * NT, v[u], gb[u], lim[u]);
+        for (int u = 0; u < 4; ++u) emit(j + u * NT, v[u], gl[u]);
     }
     for (; j < total; j += NT) {
         const uint32_t v = sorted[j];
-        emit(j, v, G[v >> tc.ts], S[v >> tc.ts]);
+        emit(j, v, GL[v >> tc.ts]);
     }
 }
 
@@ -707,7 +757,7 @@ int launch_atomic(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len
     return NB_OK;
 }
 
-template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY, int NT, bool STAGE>
+template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY, int NT, bool STAGE, int KR>
 int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                    const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st,
                    uint64_t chunk, const TileCfg &tc) {
@@ -722,7 +772,7 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, kStageBytes);
     const size_t bin_lds = (size_t)bin_sort_offset_words(tc.T) * 4 + sort_bytes;
     const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
-    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, ENTRY, NT, STAGE>;
+    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, ENTRY, NT, STAGE, KR>;
     auto tile_ow = bloom_tile_or_kernel<ENTRY, true>;
     auto tile_or = bloom_tile_or_kernel<ENTRY, false>;
     if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(tile_ow, tile_lds)) ||
@@ -744,24 +794,16 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     return NB_OK;
 }
 
-int num_cus() {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 256;
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-        return 256;
-    return n;
-}
-
-template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE>
+template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR>
 int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                  const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st) {
     constexpr uint64_t kpb = (uint64_t)KPT * NT;
     const uint64_t chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, chunk_keys(n, c.k)));
     const TileCfg tc = choose_tiles(c.fm.m, chunk, c.k);
     if (tc.ts <= 16 && env_u32("NB_ENTRY32", 0) == 0)
-        return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint16_t, NT, STAGE>(
+        return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint16_t, NT, STAGE, KR>(
             keys, offsets, key_len, n, c, words, overwrite, st, chunk, tc);
-    return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint32_t, NT, STAGE>(
+    return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint32_t, NT, STAGE, KR>(
         keys, offsets, key_len, n, c, words, overwrite, st, chunk, tc);
 }
 
@@ -772,25 +814,28 @@ int launch_build_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     const bool tiled_ok = c.k <= 32 && choose_tiles(c.fm.m, 1, c.k).T <= kMaxTiles;
     if (p == BuildPath::kAuto) p = (tiled_ok && n >= 4096) ? BuildPath::kTiled : BuildPath::kAtomic;
     if (p == BuildPath::kTiled && tiled_ok) {
-        // keys per block sized so the block's sorted indices fit in LDS
-        if (LAYOUT == kFixed16) {
+        // keys per block sized so the block's sorted indices fit in LDS; indices
+        // and their in-tile ranks kept in registers while k <= 16 (NB_RANK=0: the
+        // regenerate-and-recount variant, kept for A/B)
+        const bool rank = env_u32("NB_RANK", 1) != 0;
+        if constexpr (LAYOUT == kFixed16) {
             if (c.k <= 8)
-                return launch_tiled<FLAVOR, LAYOUT, kBinKPT, kBinThreads, false>(
+                return rank ? launch_tiled<FLAVOR, LAYOUT, kBinKPT, kBinThreads, false, 8>(
+                                  keys, offsets, key_len, n, c, words, overwrite, st)
+                            : launch_tiled<FLAVOR, LAYOUT, kBinKPT, kBinThreads, false, 0>(
+                                  keys, offsets, key_len, n, c, words, overwrite, st);
+            if (c.k <= 16 && rank)
+                return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, false, 16>(
                     keys, offsets, key_len, n, c, words, overwrite, st);
-            return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, false>(keys, offsets, key_len, n,
-                                                                       c, words, overwrite, st);
-        }
-        // variable-length keys: LDS-staged reads (default) or per-lane HBM reads
-        // (NB_VAR_MODE=0, kept for A/B: equal speed on C3, tools/varmode_gpu.sh)
-        if (env_u32("NB_VAR_MODE", 2) == 0) {
-            if (c.k <= 8)
-                return launch_tiled<FLAVOR, LAYOUT, 2, kBinThreads, false>(
+            return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, false, 0>(
+                keys, offsets, key_len, n, c, words, overwrite, st);
+        } else {  // variable-length / odd-stride keys: LDS-staged reads
+            if (c.k <= 16 && rank)
+                return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, true, 16>(
                     keys, offsets, key_len, n, c, words, overwrite, st);
-            return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, false>(keys, offsets, key_len, n,
-                                                                       c, words, overwrite, st);
+            return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, true, 0>(
+                keys, offsets, key_len, n, c, words, overwrite, st);
         }
-        return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, true>(keys, offsets, key_len, n, c,
-                                                                  words, overwrite, st);
     }
     return launch_atomic<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, overwrite, st);
 }

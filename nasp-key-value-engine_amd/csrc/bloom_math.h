@@ -73,8 +73,10 @@ inline FastMod make_fastmod(uint32_t m) {
 
 // Remainder of (u1:u0) / d, requires u1 < d, d normalized.
 NB_HD uint32_t rem_2by1(uint32_t u1, uint32_t u0, uint32_t d, uint32_t v) {
-    uint64_t q = (uint64_t)v * u1 + ((((uint64_t)u1 + 1) << 32) | u0);
-    uint32_t q1 = (uint32_t)(q >> 32), q0 = (uint32_t)q;
+    // q = v*u1 + ((u1+1) << 32 | u0) mod 2^64; v*u1 + u0 < 2^64, so the high word
+    // is hi(v*u1 + u0) + u1 + 1 (one 32x32+32 multiply-add, no 64-bit add)
+    const uint64_t p = (uint64_t)v * u1 + u0;
+    uint32_t q1 = (uint32_t)(p >> 32) + u1 + 1u, q0 = (uint32_t)p;
     uint32_t r = u0 - q1 * d;
     if (r > q0) r += d;
     if (r >= d) r -= d;
@@ -92,6 +94,14 @@ NB_HD uint32_t mod64(uint64_t x, const FastMod &f) {
 // (a + b) mod m for a, b < m without 32-bit overflow.
 NB_HD uint32_t addmod(uint32_t a, uint32_t b, uint32_t m) {
     return a >= m - b ? a - (m - b) : a + b;
+}
+// The same for any m < 2^32 in four VALU ops (add with carry, sub, min, select):
+// without a carry min(t, t - m) picks the reduced value (t - m wraps when t < m);
+// with one the true sum is t + 2^32 >= m, reduced to t - m (mod 2^32).
+NB_HD uint32_t addmod_fast(uint32_t a, uint32_t b, uint32_t m) {
+    const uint32_t t = a + b, u = t - m;
+    const uint32_t mn = t < u ? t : u;
+    return t < a ? u : mn;
 }
 NB_HD uint32_t submod(uint32_t a, uint32_t b, uint32_t m) {
     return a >= b ? a - b : a + (m - b);
@@ -161,6 +171,26 @@ inline void set_fixed_len(FilterConsts &c, uint32_t len) {
     c.fixed_len = len;
     c.h2_init_fixed = h2_state_after_prefix(c, len);
 }
+
+// Index generator of one key: r_i = (h1 + i*h2 mod 2^64) mod m, incrementally
+// (rewrite 2 above).  With s2 = (s - 2^64) mod m precomputed, a step is one
+// 64-bit add, one select on its carry and one modular add.
+struct IndexGen {
+    uint64_t x, h2;
+    uint32_t r, s, s2;  // r = current index; s = h2 mod m; s2 = (h2 - 2^64) mod m
+    NB_HD void start(uint64_t h1_, uint64_t h2_, const FilterConsts &c) {
+        x = h1_;
+        h2 = h2_;
+        r = mod64(h1_, c.fm);
+        s = mod64(h2_, c.fm);
+        s2 = submod(s, c.c64, c.fm.m);
+    }
+    NB_HD void next(const FilterConsts &c) {
+        const uint64_t nx = x + h2;
+        r = addmod_fast(r, nx < x ? s2 : s, c.fm.m);
+        x = nx;
+    }
+};
 
 
 // ------------------------------------------------- word-stream hashing ----

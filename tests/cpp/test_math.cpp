@@ -28,17 +28,20 @@ int main() {
         nb::FilterConsts c = nb::make_consts(m, 10, 17027509906831645879ull, 0);
         for (int t = 0; t < 200; ++t) {
             uint64_t h1 = rng(), h2 = rng();
-            uint32_t r = nb::mod64(h1, c.fm), s = nb::mod64(h2, c.fm);
-            uint64_t x = h1;
+            if (t == 0) h1 = ~0ull, h2 = ~0ull;  // a wrap on every step
+            if (t == 1) h1 = 0, h2 = 1ull << 63;
+            nb::IndexGen g;  // the kernels' generator
+            g.start(h1, h2, c);
             for (uint32_t i = 0; i < 40; ++i) {
-                if (i) {
-                    uint64_t nx = x + h2;
-                    r = nb::addmod(r, s, m);
-                    if (nx < x) r = nb::submod(r, c.c64, m);
-                    x = nx;
-                }
-                if (r != (uint32_t)((h1 + (uint64_t)i * h2) % m)) ++bad;
+                if (i) g.next(c);
+                if (g.r != (uint32_t)((h1 + (uint64_t)i * h2) % m)) ++bad;
             }
+        }
+        // modular add of the index step, including sums that carry out of 32 bits
+        for (int t = 0; t < 2000; ++t) {
+            uint32_t a = (uint32_t)(rng() % m), b = (uint32_t)(rng() % m);
+            if (t == 0) a = b = m - 1;
+            if (nb::addmod_fast(a, b, m) != (uint32_t)(((uint64_t)a + b) % m)) ++bad;
         }
     }
     printf("mod/incremental mismatches: %ld\n", bad);
