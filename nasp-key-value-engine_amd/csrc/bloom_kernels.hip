@@ -54,7 +54,35 @@ __device__ __forceinline__ void key_hashes_ptr(const FilterConsts &c, const uint
     nb::hash_aligned_words<FLAVOR, decltype(load), FIXED_LEN>(c, load, a, len, h1, h2);
 }
 
+// libstdc++ hashes of a 16-byte key with PREM = D % 8 leftover seed digits, as
+// straight-line code: h2's stream is the PREM digits ++ the key, i.e. two whole
+// words spliced with constant funnel shifts and (PREM > 0) a PREM-byte tail --
+// the same words lsx_begin_fixed/lsx_consume/lsx_end feed, without their
+// run-time shift amounts and branches.
+template <int PREM>
+__device__ __forceinline__ void lsx16(const FilterConsts &c, const ulonglong2 &kv, uint64_t *h1,
+                                      uint64_t *h2) {
+    uint64_t h = nb::lsx_init(16);
+    h = nb::lsx_round(h, kv.x);
+    h = nb::lsx_round(h, kv.y);
+    *h1 = nb::lsx_final(h);
+    uint64_t g = c.h2_init_fixed;
+    if (PREM == 0) {
+        g = nb::lsx_round(g, kv.x);
+        g = nb::lsx_round(g, kv.y);
+    } else {
+        constexpr int r8 = 8 * PREM;
+        g = nb::lsx_round(g, c.pre_tail | (kv.x << r8));
+        g = nb::lsx_round(g, (kv.x >> (64 - r8)) | (kv.y << r8));
+        g = nb::lsx_tail(g, kv.y >> (64 - r8));
+    }
+    *h2 = nb::lsx_final(g);
+}
+
 // Fixed 16-byte keys, 16-byte aligned: one dwordx4 load per lane.
+#ifndef NB_PREM_SPECIALIZE
+#define NB_PREM_SPECIALIZE 1
+#endif
 template <int FLAVOR>
 __device__ __forceinline__ void hash16(const FilterConsts &c, const ulonglong2 &kv, uint64_t *h1,
                                        uint64_t *h2) {
@@ -64,12 +92,23 @@ __device__ __forceinline__ void hash16(const FilterConsts &c, const ulonglong2 &
         nb::fnv_consume(f1, f2, kv.y, 8);
         *h1 = f1;
         *h2 = f2;
-    } else {
+    } else if (!NB_PREM_SPECIALIZE) {
         LsxState s;
         nb::lsx_begin_fixed(c, s, 16);
         nb::lsx_consume(c, s, 0, kv.x, 16);
         nb::lsx_consume(c, s, 1, kv.y, 16);
         nb::lsx_end(c, s, 16, h1, h2);
+    } else {
+        switch (c.prem) {  // kernel-uniform: a scalar branch
+            case 0: lsx16<0>(c, kv, h1, h2); break;
+            case 1: lsx16<1>(c, kv, h1, h2); break;
+            case 2: lsx16<2>(c, kv, h1, h2); break;
+            case 3: lsx16<3>(c, kv, h1, h2); break;
+            case 4: lsx16<4>(c, kv, h1, h2); break;
+            case 5: lsx16<5>(c, kv, h1, h2); break;
+            case 6: lsx16<6>(c, kv, h1, h2); break;
+            default: lsx16<7>(c, kv, h1, h2); break;
+        }
     }
 }
 
@@ -276,9 +315,129 @@ struct TileScratch {
     uint32_t *spill32;    // [2*ceil(m/64)] spill bitmap (zero between builds)
 };
 
+// Phases 2-4 of the bin kernel in rank mode when T <= 2 NT: thread tid owns the
+// two tiles 2 tid, 2 tid + 1 from the scan to the run table, so the scan is one
+// wave-scan round (no per-thread loops) and the reservations use the counts it
+// already holds.  Addresses are precomputed where the hot loops use them: the run
+// starts as byte offsets of `sorted` (placement = one shift-add per index) and the
+// run table as byte offsets into the buckets (write-out = one add per entry, a
+// 32-bit offset from the buckets' base) while the buckets stay under 4 GiB.
+template <int NT, int KPT, int KR, typename ENTRY>
+__device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_off_words,
+                                                   const TileCfg &tc, const TileScratch &sc,
+                                                   ENTRY *__restrict__ buckets, uint64_t base,
+                                                   uint64_t n, uint32_t k,
+                                                   const uint32_t (&ridx)[KPT][KR],
+                                                   const uint32_t (&rank)[KPT][KR]) {
+    constexpr uint32_t kWaves = NT / 64;
+    const uint32_t T = tc.T, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    uint32_t *cnt = lds;                  // [T] counts; then the run table
+    uint32_t *S4 = lds + T;               // [T] run starts, byte offsets from lds
+    uint32_t *wave_sums = lds + 2 * T;    // [kWaves + 1]
+    char *lds_b = reinterpret_cast<char *>(lds);
+    const uint32_t sort_b = sort_off_words * 4;
+    // ---- phase 2: scan (one round), reservations
+    const uint32_t t0 = 2 * tid;
+    uint32_t h0 = 0, h1 = 0;
+    if (t0 + 1 < T) {
+        const uint2 hh = *reinterpret_cast<const uint2 *>(cnt + t0);
+        h0 = hh.x;
+        h1 = hh.y;
+    } else if (t0 < T) {
+        h0 = cnt[t0];
+    }
+    const uint32_t local = h0 + h1;
+    const uint32_t incl = wave_inclusive_scan(local);
+    if (lane == 63) wave_sums[wid] = incl;
+    __syncthreads();
+    if (wid == 0) {
+        const uint32_t w = lane < kWaves ? wave_sums[lane] : 0;
+        const uint32_t wi = wave_inclusive_scan(w);
+        if (lane < kWaves) wave_sums[lane] = wi - w;
+        if (lane == kWaves - 1) wave_sums[kWaves] = wi;
+    }
+    __syncthreads();
+    const uint32_t st0 = wave_sums[wid] + incl - local, st1 = st0 + h0;
+    const uint32_t total = wave_sums[kWaves];
+    const uint32_t shard = blockIdx.x % tc.G;
+    uint32_t *cur = sc.gcur + (size_t)shard * T;
+    const uint32_t g0 = h0 ? atomicAdd(&cur[t0], h0) : 0u;
+    const uint32_t g1 = h1 ? atomicAdd(&cur[t0 + 1], h1) : 0u;
+    if (t0 < T) S4[t0] = sort_b + 4 * st0;  // (S4 + t0 is 8-byte aligned only for even T)
+    if (t0 + 1 < T) S4[t0 + 1] = sort_b + 4 * st1;
+    __syncthreads();
+    if (NB_DIAG_STOP(2)) return;
+    // ---- phase 3: placement (the reservations' round trips overlap it)
+#pragma unroll
+    for (int p = 0; p < KPT; ++p) {
+        if (base + (uint64_t)p * NT + tid < n) {
+#pragma unroll
+            for (int j = 0; j < KR; ++j)
+                if (j < (int)k)
+                    *reinterpret_cast<uint32_t *>(lds_b + S4[ridx[p][j] >> tc.ts] + 4 * rank[p][j]) =
+                        ridx[p][j];
+        }
+    }
+    const int ovf = ((uint64_t)g0 + h0 > tc.cap) | ((uint64_t)g1 + h1 > tc.cap);
+    const bool any_ovf = __syncthreads_or(ovf) != 0;  // cnt and S4 are dead now
+    // run table: first-entry index minus the run's local start (wrapping u32), in
+    // bytes when the buckets fit 32-bit offsets; limits over S4 on overflow
+    const bool b32 = (uint64_t)T * tc.G * tc.cap * sizeof(ENTRY) <= 0xFFFFFFFFull;
+    const uint32_t esz = (b32 && !any_ovf) ? (uint32_t)sizeof(ENTRY) : 1u;
+    if (t0 < T) {
+        cnt[t0] = ((t0 * tc.G + shard) * tc.cap + g0 - st0) * esz;
+        if (any_ovf) S4[t0] = st0 + (g0 < tc.cap ? tc.cap - g0 : 0u);
+    }
+    if (t0 + 1 < T) {
+        cnt[t0 + 1] = (((t0 + 1) * tc.G + shard) * tc.cap + g1 - st1) * esz;
+        if (any_ovf) S4[t0 + 1] = st1 + (g1 < tc.cap ? tc.cap - g1 : 0u);
+    }
+    __syncthreads();
+    if (NB_DIAG_STOP(3)) return;
+    // ---- phase 4: coalesced write-out, four independent entries per lane per step
+    const uint32_t *sorted = lds + sort_off_words;
+    const uint32_t *GX = cnt;
+    if (!any_ovf && b32) {
+        char *bb = reinterpret_cast<char *>(buckets);
+        uint32_t j = tid;
+        for (; j + 3 * NT < total; j += 4 * NT) {
+            uint32_t v[4], g[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) g[u] = GX[v[u] >> tc.ts];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                *reinterpret_cast<ENTRY *>(bb + (g[u] + (j + u * NT) * (uint32_t)sizeof(ENTRY))) =
+                    (ENTRY)v[u];
+        }
+        for (; j < total; j += NT) {
+            const uint32_t v = sorted[j];
+            *reinterpret_cast<ENTRY *>(bb + (GX[v >> tc.ts] + j * (uint32_t)sizeof(ENTRY))) = (ENTRY)v;
+        }
+    } else {
+        // 64-bit entry addresses; on overflow entries past a bucket's capacity go
+        // to the spill bitmap
+        for (uint32_t j = tid; j < total; j += NT) {
+            const uint32_t v = sorted[j], t = v >> tc.ts;
+            if (!any_ovf || j < S4[t]) {
+                buckets[(uint32_t)(GX[t] + j)] = (ENTRY)v;
+            } else {
+                __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+                sc.spill_flag[t] = 1u;
+            }
+        }
+    }
+}
+
+// Two resident blocks per CU (8 waves per SIMD at NT = 1024): <= 64 VGPRs.
+#ifndef NB_BIN_MIN_WAVES
+#define NB_BIN_MIN_WAVES(NT) (2 * (NT) / 256)
+#endif
 template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY, int NT = kBinThreads,
           bool STAGE = (LAYOUT != kFixed16), int KR = 0>
-__global__ __launch_bounds__(NT) void bloom_bin_kernel(
+__global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
     uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc, ENTRY *__restrict__ buckets) {
     extern __shared__ uint32_t lds[];
@@ -382,6 +541,11 @@ __global__ __launch_bounds__(NT) void bloom_bin_kernel(
     }
     __syncthreads();
     if (NB_DIAG_STOP(1)) return;
+    if (KR > 0 && T <= 2 * NT) {  // block-uniform: the common case (e.g. C2's 1 463 tiles)
+        bin_tail_two_tiles<NT, KPT, kR>(lds, bin_sort_offset_words(T), tc, sc, buckets, base, n,
+                                        c.k, ridx, rank);
+        return;
+    }
 
     // phase 2: block-local run starts; reserve a run in every touched tile's
     // bucket shard (cursor shard = blockIdx % G, laid out [shard][tile]).  Per tile
@@ -393,21 +557,23 @@ __global__ __launch_bounds__(NT) void bloom_bin_kernel(
     uint32_t *cur = sc.gcur + (size_t)shard * T;
     // tiles owned by this thread in phase 2: t = tid + u*NT
     constexpr int kTPT = (kMaxTiles + NT - 1) / NT;
-    uint32_t gres[kTPT], gl_g[kTPT], gl_l[kTPT];
+    uint32_t gres[kTPT], hcnt[kTPT], gl_g[kTPT], gl_l[kTPT];
 #pragma unroll
     for (int u = 0; u < kTPT; ++u) {
         const uint32_t t = tid + u * NT;
-        const uint32_t h = t < T ? cnt[t] : 0u;
-        gres[u] = h ? atomicAdd(&cur[t], h) : 0u;
+        hcnt[u] = t < T ? cnt[t] : 0u;
+        gres[u] = hcnt[u] ? atomicAdd(&cur[t], hcnt[u]) : 0u;
     }
     if (NB_DIAG_STOP(2)) return;
     // The {G, limit} pair of a tile: G = global entry index of the block's run
     // minus its local start (u32 wrap-around), limit = first local position past
-    // the bucket's capacity.
+    // the bucket's capacity.  `ovf` notes a run that does not fit its bucket.
+    int ovf = 0;
     auto run_pair = [&](int u, uint32_t t) {
         const uint32_t st = S[t], g = gres[u];
         gl_g[u] = (t * tc.G + shard) * tc.cap + g - st;
         gl_l[u] = st + (g < tc.cap ? tc.cap - g : 0u);
+        ovf |= (uint64_t)g + hcnt[u] > tc.cap;
     };
     if (KR > 0) {
         // phase 3, rank mode: each index goes to its tile's run start + rank; the
@@ -463,18 +629,43 @@ __global__ __launch_bounds__(NT) void bloom_bin_kernel(
             }
         }
     }
-    __syncthreads();  // cnt and S are dead: the pairs go over them
+    // cnt and S are dead: the run table goes over them.  Every run fits its bucket
+    // unless the input is pathological (massively duplicated keys): then the
+    // table holds {G, limit} pairs and the write-out checks each entry.
+    const bool any_ovf = __syncthreads_or(ovf) != 0;  // block-uniform
+    uint32_t *GX = lds;  // [T] G only, when nothing overflows
 #pragma unroll
     for (int u = 0; u < kTPT; ++u) {
         const uint32_t t = tid + u * NT;
-        if (t < T) GL[t] = make_uint2(gl_g[u], gl_l[u]);
+        if (t < T) {
+            if (any_ovf) GL[t] = make_uint2(gl_g[u], gl_l[u]);
+            else GX[t] = gl_g[u];
+        }
     }
     __syncthreads();
     if (NB_DIAG_STOP(3)) return;
 
-    // phase 4: coalesced write-out of the runs (spill beyond capacity), four
-    // independent entries per lane per step so the LDS lookups overlap.  Entries
-    // are stored unmasked (a u16 store keeps the low bits; the tile kernel masks).
+    // phase 4: coalesced write-out of the runs, four independent entries per
+    // lane per step so the LDS lookups overlap.  Entries are stored unmasked (a
+    // u16 store keeps the low bits; the tile kernel masks).
+    if (!any_ovf) {
+        uint32_t j = tid;
+        for (; j + 3 * NT < total; j += 4 * NT) {
+            uint32_t v[4], g[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) g[u] = GX[v[u] >> tc.ts];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) buckets[g[u] + j + u * NT] = (ENTRY)v[u];
+        }
+        for (; j < total; j += NT) {
+            const uint32_t v = sorted[j];
+            buckets[GX[v >> tc.ts] + j] = (ENTRY)v;
+        }
+        return;
+    }
+    // slow path: entries past a bucket's capacity go to the spill bitmap
     auto emit = [&](uint32_t j, uint32_t v, uint2 gl) {
         if (j < gl.y) {
             buckets[gl.x + j] = (ENTRY)v;
@@ -784,8 +975,8 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         const uint64_t cn = std::min(chunk, n - done);
         const uint8_t *ck = offsets ? keys : keys + done * key_len;
         const uint64_t *co = offsets ? offsets + done : nullptr;
-        hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds,
-                           st, ck, co, key_len, cn, c, tc, sc, bk);
+        hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st, ck,
+                           co, key_len, cn, c, tc, sc, bk);
         NB_HIP(hipGetLastError());
         hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(tc.T),
                            dim3(kTileThreads), tile_lds, st, tc, sc, bk, words, nwords);

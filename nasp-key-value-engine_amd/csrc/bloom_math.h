@@ -173,21 +173,25 @@ inline void set_fixed_len(FilterConsts &c, uint32_t len) {
 }
 
 // Index generator of one key: r_i = (h1 + i*h2 mod 2^64) mod m, incrementally
-// (rewrite 2 above).  With s2 = (s - 2^64) mod m precomputed, a step is one
-// 64-bit add, one select on its carry and one modular add.
+// (rewrite 2 above).  The two step sizes s = h2 mod m and s2 = (h2 - 2^64) mod m
+// are kept biased by -m (mod 2^32): r + (a - m) carries out of 32 bits exactly
+// when r + a >= m, so a step is one 64-bit add, one select on its carry, and a
+// modular add of three ops (add with carry-out, add m, select) for any m < 2^32.
 struct IndexGen {
     uint64_t x, h2;
-    uint32_t r, s, s2;  // r = current index; s = h2 mod m; s2 = (h2 - 2^64) mod m
+    uint32_t r, sb, s2b;  // r = current index; sb = s - m, s2b = s2 - m (mod 2^32)
     NB_HD void start(uint64_t h1_, uint64_t h2_, const FilterConsts &c) {
         x = h1_;
         h2 = h2_;
         r = mod64(h1_, c.fm);
-        s = mod64(h2_, c.fm);
-        s2 = submod(s, c.c64, c.fm.m);
+        const uint32_t s = mod64(h2_, c.fm);
+        sb = s - c.fm.m;
+        s2b = submod(s, c.c64, c.fm.m) - c.fm.m;
     }
     NB_HD void next(const FilterConsts &c) {
         const uint64_t nx = x + h2;
-        r = addmod_fast(r, nx < x ? s2 : s, c.fm.m);
+        const uint32_t t = r + (nx < x ? s2b : sb);
+        r = t < r ? t : t + c.fm.m;  // carry: r + a >= m, t = r + a - m
         x = nx;
     }
 };
