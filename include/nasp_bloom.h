@@ -87,6 +87,32 @@ int nb_probe(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uin
              uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
              const uint64_t *words, uint8_t *out, int device);
 
+/* ---------------------------------------------- streaming host builder --- */
+/* The host side of SSTable::build's filter block (SSTable/SSTable.cpp:28-35):
+ * keys arrive one at a time from the flushing memtable / compaction merge
+ * (MemtableManager.cpp:109-130, LSMManager.cpp:42-90) and BloomFilter::add
+ * (BloomFilter.cpp:82-86) is called per key.  A builder packs the keys into a
+ * ring of pinned host chunks; every full chunk is uploaded asynchronously and
+ * built on the device (OR-accumulated into the device-resident filter) while the
+ * caller keeps packing the next one, so packing, PCIe and the build overlap.
+ * Chunks whose keys all have one length travel without offsets.
+ * Not thread-safe (one builder per caller thread, like the reference class). */
+typedef struct nb_builder nb_builder;
+/* init_words: ceil(m/64) host words the keys are OR-ed into (the add-after-
+ * deserialize semantics, TypesManager.cpp:84-86), or NULL for a fresh filter. */
+int nb_builder_create(uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
+                      const uint64_t *init_words, int device, nb_builder **out);
+/* BloomFilter::add of one key (any bytes, len may be 0). */
+int nb_builder_add(nb_builder *b, const uint8_t *key, uint64_t len);
+/* Many keys (same packing as nb_build): uploaded chunk by chunk straight from
+ * the caller's buffer, each chunk's build overlapping the next chunk's upload. */
+int nb_builder_add_batch(nb_builder *b, const uint8_t *keys, const uint64_t *offsets,
+                         uint32_t key_len, uint64_t n);
+/* Build everything added so far and copy the filter to `words` (ceil(m/64) host
+ * words).  The builder stays usable: later adds OR into the same filter. */
+int nb_builder_finish(nb_builder *b, uint64_t *words);
+int nb_builder_destroy(nb_builder *b);
+
 /* ------------------------------------------ device-resident entry points --- */
 /* Same contracts; every pointer is device memory on the current device and
  * the work is enqueued on `stream` (a hipStream_t; NULL = the null stream).

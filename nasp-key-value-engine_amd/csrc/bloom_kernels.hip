@@ -1138,6 +1138,16 @@ size_t keys_bytes(const uint64_t *offsets, uint32_t key_len, uint64_t n) {
 
 }  // namespace
 
+// Internal entry points for the other translation units of the library
+// (bloom_stream.cpp): the device build on a caller's stream, and the error slot.
+int nb_internal_build(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
+                      uint64_t n, uint32_t m, uint32_t k, uint64_t seed, int flavor,
+                      uint64_t *d_words, bool overwrite, hipStream_t st) {
+    return launch_build(d_keys, d_offsets, key_len, n, m, k, seed, flavor, d_words, overwrite, st);
+}
+int nb_internal_fail(int code, const char *msg) { return fail(code, msg); }
+void nb_internal_stream_shutdown();  // bloom_stream.cpp: releases the builders' slot pool
+
 // =================================================================== C ABI ==
 
 extern "C" {
@@ -1164,6 +1174,7 @@ int nb_shutdown(void) {
         }
         g_ws.clear();
     }
+    nb_internal_stream_shutdown();
     for (int i = 0; i < kMaxDev; ++i) {
         DevScratch &d = g_dev[i];
         std::lock_guard<std::mutex> lk(d.mu);
@@ -1197,26 +1208,15 @@ uint64_t nb_seed_from_time(uint32_t time_const);  // defined in bloom_host.cpp
 
 int nb_build(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
              uint32_t m, uint32_t k, uint64_t h2_seed, int flavor, uint64_t *words, int device) {
+    // the streaming builder (bloom_stream.cpp): the current words go up once,
+    // the keys chunk by chunk with every chunk's build overlapping the next upload
     int rc = check_common(n, m, flavor, keys, words);
     if (rc || n == 0 || k == 0) return rc;
-    DevScratch *d;
-    if ((rc = open_device(device, &d))) return rc;
-    std::lock_guard<std::mutex> lk(d->mu);
-    const size_t kb = keys_bytes(offsets, key_len, n);
-    const size_t wb = nwords_of(m) * 8;
-    if ((rc = ensure(*d, 0, kb + 16)) || (offsets && (rc = ensure(*d, 1, (n + 1) * 8))) ||
-        (rc = ensure(*d, 2, wb)))
-        return rc;
-    NB_HIP(hipMemcpyAsync(d->buf[0], keys, kb, hipMemcpyHostToDevice, d->stream));
-    if (offsets)
-        NB_HIP(hipMemcpyAsync(d->buf[1], offsets, (n + 1) * 8, hipMemcpyHostToDevice, d->stream));
-    NB_HIP(hipMemcpyAsync(d->buf[2], words, wb, hipMemcpyHostToDevice, d->stream));
-    rc = launch_build((const uint8_t *)d->buf[0], offsets ? (const uint64_t *)d->buf[1] : nullptr,
-                      key_len, n, m, k, h2_seed, flavor, (uint64_t *)d->buf[2], false, d->stream);
-    if (rc) return rc;
-    NB_HIP(hipMemcpyAsync(words, d->buf[2], wb, hipMemcpyDeviceToHost, d->stream));
-    NB_HIP(hipStreamSynchronize(d->stream));
-    return NB_OK;
+    nb_builder *b = nullptr;
+    if ((rc = nb_builder_create(m, k, h2_seed, flavor, words, device, &b))) return rc;
+    if (!(rc = nb_builder_add_batch(b, keys, offsets, key_len, n))) rc = nb_builder_finish(b, words);
+    const int rd = nb_builder_destroy(b);
+    return rc ? rc : rd;
 }
 
 int nb_probe(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,

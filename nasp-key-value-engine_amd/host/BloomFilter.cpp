@@ -43,30 +43,77 @@ unsigned int BloomFilter::calculateNumberOfHashFunctions(unsigned int expectedEl
     return nb_num_hashes(expectedElements, mm);
 }
 
-// BloomFilter.cpp:82-86, batched: the key bytes are appended, built later on the GPU.
+BloomFilter::BloomFilter(const BloomFilter &o)
+    : m(o.m), k(o.k), p(o.p), timeConst(o.timeConst), h2_seed(o.h2_seed), closures(o.closures),
+      flavor(o.flavor), device(o.device) {
+    o.flush();
+    bits = o.bits;
+    bits_zero = o.bits_zero;
+}
+
+BloomFilter &BloomFilter::operator=(const BloomFilter &o) {
+    if (this == &o) return *this;
+    o.flush();
+    release();
+    m = o.m; k = o.k; p = o.p; timeConst = o.timeConst; h2_seed = o.h2_seed;
+    closures = o.closures; flavor = o.flavor; device = o.device;
+    bits = o.bits;
+    bits_zero = o.bits_zero;
+    return *this;
+}
+
+BloomFilter::BloomFilter(BloomFilter &&o) noexcept
+    : m(o.m), k(o.k), p(o.p), bits(std::move(o.bits)), timeConst(o.timeConst),
+      h2_seed(o.h2_seed), closures(o.closures), flavor(o.flavor), device(o.device),
+      builder(o.builder), bits_zero(o.bits_zero) {
+    o.builder = nullptr;
+}
+
+BloomFilter &BloomFilter::operator=(BloomFilter &&o) noexcept {
+    if (this == &o) return *this;
+    release();
+    m = o.m; k = o.k; p = o.p; timeConst = o.timeConst; h2_seed = o.h2_seed;
+    closures = o.closures; flavor = o.flavor; device = o.device;
+    bits = std::move(o.bits);
+    bits_zero = o.bits_zero;
+    builder = o.builder;
+    o.builder = nullptr;
+    return *this;
+}
+
+BloomFilter::~BloomFilter() { release(); }
+
+void BloomFilter::release() noexcept {
+    if (builder) (void)nb_builder_destroy(builder);  // pending keys are dropped with the object
+    builder = nullptr;
+}
+
+// BloomFilter.cpp:82-86: the key is packed into the streaming builder; its chunk
+// is uploaded and built on the GPU while later keys are packed.
 void BloomFilter::add(const std::string &elem) {
-    if (pend_offs.empty()) pend_offs.push_back(0);
-    pend_bytes.insert(pend_bytes.end(), elem.begin(), elem.end());
-    pend_offs.push_back(pend_bytes.size());
-    if (pend_offs.size() - 1 >= kBatchKeys) flush();
+    if (!closures || k == 0) return;  // no hash closures: nothing to set
+    if (m == 0) throw std::runtime_error("nasp_bloom: add() on a filter with m == 0");
+    if (!builder)
+        check(nb_builder_create(m, k, h2_seed, flavor, bits_zero ? nullptr : bits.data(), device,
+                                &builder),
+              "nb_builder_create");
+    check(nb_builder_add(builder, reinterpret_cast<const uint8_t *>(elem.data()), elem.size()),
+          "nb_builder_add");
 }
 
 void BloomFilter::addBatch(const std::vector<std::string> &elems) {
     for (const std::string &e : elems) add(e);
 }
 
+// Materialise: download the filter the builder holds, return its buffers.
 void BloomFilter::flush() const {
-    if (pend_offs.size() < 2) return;
-    const uint64_t n = pend_offs.size() - 1;
-    if (closures && k > 0) {
-        if (m == 0) throw std::runtime_error("nasp_bloom: add() on a filter with m == 0");
-        pend_bytes.resize(pend_bytes.size() + 16, 0);  // slack for aligned device loads
-        check(nb_build(pend_bytes.data(), pend_offs.data(), 0, n, m, k, h2_seed, flavor,
-                       bits.data(), device),
-              "nb_build");
-    }
-    pend_bytes.clear();
-    pend_offs.clear();
+    if (!builder) return;
+    nb_builder *b = builder;
+    builder = nullptr;
+    const int rc = nb_builder_finish(b, bits.data());
+    (void)nb_builder_destroy(b);
+    check(rc, "nb_builder_finish");
+    bits_zero = false;
 }
 
 // BloomFilter.cpp:67-80 for one key, on the host against the same bits.
@@ -108,6 +155,7 @@ BloomFilter BloomFilter::deserialize(const std::vector<std::byte> &data) {
     bf.timeConst = tc;
     bf.h2_seed = seed;
     bf.bits.assign(((size_t)mm + 63) / 64, 0);
+    bf.bits_zero = false;
     if (!bf.bits.empty())
         check(nb_deserialize(img, data.size(), nullptr, nullptr, nullptr, nullptr, nullptr,
                              bf.bits.data()),

@@ -9,10 +9,11 @@
 // What changes inside:
 //   - the bit set is a std::vector<uint64_t> (little-endian words == the
 //     serialized LSB-first byte image) instead of vector<bool>;
-//   - add() appends the key to a packed batch (bytes + offsets); the batch is
-//     built on the GPU in one call (nb_build, include/nasp_bloom.h) when the
-//     filter is next read (possiblyContains / serialize / copy) or when it grows
-//     past kBatchKeys;
+//   - add() packs the key into a streaming builder (nb_builder_*, include/
+//     nasp_bloom.h): pinned host chunks whose upload and device build overlap the
+//     packing of the next keys; the filter is downloaded when it is next read
+//     (possiblyContains / serialize / copy), which also returns the builder's
+//     buffers to the library's pool;
 //   - possiblyContains() of one key is evaluated on the host against the same
 //     bits (the latency-bound lookup path, SSTManager.cpp:203,224), with the
 //     exact same index arithmetic the kernels use (csrc/bloom_math.h).
@@ -49,18 +50,25 @@ private:
 
     int flavor;                 // std::hash flavour (NB_FLAVOR_*)
     int device = 0;
-    // pending batch of added keys (materialised lazily; mutable for const readers)
-    mutable std::vector<uint8_t> pend_bytes;
-    mutable std::vector<uint64_t> pend_offs;  // n+1 offsets (empty when no keys)
+    // keys added since the last read, in flight on the device (mutable: const
+    // readers materialise them); bits_zero: `bits` is still all zero
+    mutable struct nb_builder *builder = nullptr;
+    mutable bool bits_zero = true;
 
     void flush() const;
+    void release() noexcept;
 
 public:
-    static constexpr size_t kBatchKeys = size_t(1) << 22;
-
     // Constructor
     BloomFilter();
     BloomFilter(unsigned int n, double falsePositiveRate);
+    // Copyable and assignable like the reference class (SSTable.cpp:35 assigns
+    // the built filter): a copy materialises the source's pending keys first.
+    BloomFilter(const BloomFilter &o);
+    BloomFilter &operator=(const BloomFilter &o);
+    BloomFilter(BloomFilter &&o) noexcept;
+    BloomFilter &operator=(BloomFilter &&o) noexcept;
+    ~BloomFilter();
 
     // Add an element to the Bloom Filter
     void add(const std::string& elem);

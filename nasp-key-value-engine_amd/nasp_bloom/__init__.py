@@ -6,11 +6,13 @@ is the Python binding used by tests/ and bench.py:
 
   build_device / probe_device  -- device-resident batch build / probe on torch tensors
   build_host / probe_host      -- host-buffer entry points (H2D + kernel + D2H)
+  Builder                      -- streaming host builder: pinned chunks, packing /
+                                  upload / device build overlapped (nb_builder_*)
   BloomFilter                  -- mirror of the reference class surface
                                   (reference BloomFilter/BloomFilter.h:24-41)
   distributed                  -- multi-GPU: independent filters / cooperative OR-merge
 """
 from ._lib import (FLAVOR_LIBSTDCXX, FLAVOR_MSVC_FNV1A, NaspBloomError, lib)  # noqa: F401
-from .api import (BloomFilter, build_device, build_host, deserialize, nwords, or_merge_device,  # noqa: F401
+from .api import (BloomFilter, Builder, build_device, build_host, deserialize, nwords, or_merge_device,  # noqa: F401
                   probe_device, probe_host, seed_from_time, serialize, size_of_bitset,
                   num_hashes)

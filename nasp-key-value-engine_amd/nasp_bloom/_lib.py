@@ -57,6 +57,13 @@ _SIGS = {
     "nb_frame_filter_device": (C.c_int, [C.c_uint32, C.c_uint32, C.c_double, C.c_uint32,
                                          C.c_uint64, C.c_void_p, C.c_int, C.c_uint32,
                                          C.c_void_p, C.c_void_p]),
+    "nb_builder_create": (C.c_int, [C.c_uint32, C.c_uint32, C.c_uint64, C.c_int, C.c_void_p,
+                                    C.c_int, C.POINTER(C.c_void_p)]),
+    "nb_builder_add": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    "nb_builder_add_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                       C.c_uint64]),
+    "nb_builder_finish": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "nb_builder_destroy": (C.c_int, [C.c_void_p]),
 }
 
 FRAME_RAW = 0

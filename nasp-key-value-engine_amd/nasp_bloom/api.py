@@ -104,6 +104,51 @@ def probe_host(keys: np.ndarray, offsets: np.ndarray | None, key_len: int, n: in
     return out[:n]
 
 
+class Builder:
+    """Streaming host builder (nb_builder_*): keys packed into pinned chunks whose
+    upload and device build overlap further packing; finish() returns the filter
+    words.  init_words: host words the keys OR into (None = a fresh filter)."""
+
+    def __init__(self, m: int, k: int, seed: int, flavor: int = FLAVOR_LIBSTDCXX,
+                 init_words: np.ndarray | None = None, device: int = 0):
+        self.m = m
+        self._h = C.c_void_p()
+        if init_words is not None:
+            assert init_words.dtype == np.uint64 and init_words.size >= nwords(m)
+        check(lib().nb_builder_create(m, k, seed, flavor, _np_ptr(init_words), device,
+                                      C.byref(self._h)), "nb_builder_create")
+
+    def add(self, key: bytes) -> None:
+        check(lib().nb_builder_add(self._h, key, len(key)), "nb_builder_add")
+
+    def add_batch(self, keys: np.ndarray, offsets: np.ndarray | None, key_len: int, n: int) -> None:
+        check(lib().nb_builder_add_batch(self._h, _np_ptr(keys), _np_ptr(offsets), key_len, n),
+              "nb_builder_add_batch")
+
+    def finish(self, words: np.ndarray | None = None) -> np.ndarray:
+        if words is None:
+            words = np.zeros(max(nwords(self.m), 1), dtype=np.uint64)
+        check(lib().nb_builder_finish(self._h, _np_ptr(words)), "nb_builder_finish")
+        return words
+
+    def close(self) -> None:
+        if self._h:
+            check(lib().nb_builder_destroy(self._h), "nb_builder_destroy")
+            self._h = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+
 def serialize(m: int, k: int, p: float, time_const: int, seed: int, words: np.ndarray) -> bytes:
     size = lib().nb_serialized_size(m)
     out = np.zeros(size, dtype=np.uint8)
