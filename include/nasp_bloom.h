@@ -68,6 +68,9 @@ int nb_shutdown(void);
 uint32_t nb_size_of_bitset(uint32_t n, double p);
 /* BloomFilter::calculateNumberOfHashFunctions (BloomFilter.cpp:196-199). */
 uint32_t nb_num_hashes(uint32_t n, uint32_t m);
+/* std::hash<std::string> of `len` bytes in the selected flavour (host only): the
+ * reference's h1 (BloomFilter.cpp:59) and MerkleTree::hash (merkle.cpp:26-32). */
+uint64_t nb_std_hash(const uint8_t *p, uint64_t len, int flavor);
 /* h2_seed from timeConst: mt19937(timeConst) + uniform_int_distribution<uint64_t>
  * (BloomFilter.cpp:37,44-46). */
 uint64_t nb_seed_from_time(uint32_t time_const);
@@ -142,6 +145,24 @@ int nb_probe_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t k
  * of the cooperative multi-GPU build (RCCL has no bitwise-OR reduction). */
 int nb_or_merge_device(uint64_t *d_dst, const uint64_t *d_src, uint64_t nwords,
                        uint32_t nsrc, uint64_t src_stride, void *stream);
+
+/* ------------------------------------------------------------ Merkle tree --- */
+/* The Merkle tree SSTable::build makes on the same flush (SSTable/SSTable.cpp:29-40;
+ * SSTableRaw.cpp:238,392-397 over key ++ value), replacing MerkleTree(data)
+ * (MerkleTree/merkle.cpp:7-55).  Records are packed like keys (offsets, or a fixed
+ * rec_len).  The tree holds every level as std::hash values, leaves first, root
+ * last: leaves[i] = H(record i); a parent is H(to_string(left) ++ to_string(right)),
+ * the last node of an odd level paired with itself; the reference's strings are
+ * the decimal forms of these values (getLeaves(), getRootHash(), and the
+ * treeLevels generateProof walks).  n == 0 is NB_ERR_ARG (the reference throws). */
+uint64_t nb_merkle_tree_size(uint64_t n);  /* n + ceil(n/2) + ... + 1 */
+/* d_tree: nb_merkle_tree_size(n) device words; asynchronous on `stream`. */
+int nb_merkle_device(const uint8_t *d_data, const uint64_t *d_offsets, uint32_t rec_len,
+                     uint64_t n, int flavor, uint64_t *d_tree, void *stream);
+/* Host buffers: tree (nb_merkle_tree_size(n) words) and leaves (n words) may be
+ * NULL; *root always receives the root hash. */
+int nb_merkle(const uint8_t *data, const uint64_t *offsets, uint32_t rec_len, uint64_t n,
+              int flavor, uint64_t *tree, uint64_t *leaves, uint64_t *root, int device);
 
 /* ------------------------------------------------------ serialization --- */
 /* Size of BloomFilter::serialize()'s image: 28 + (uint32_t)(m+7)/8 bytes

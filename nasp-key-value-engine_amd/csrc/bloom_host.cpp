@@ -4,12 +4,14 @@
 //   nb_seed_from_time  <- BloomFilter.cpp:37,44-46 (mt19937 + uniform_int_distribution)
 //   nb_serialize       <- BloomFilter.cpp:88-129
 //   nb_deserialize     <- BloomFilter.cpp:131-190
+//   nb_std_hash        <- std::hash<std::string> (BloomFilter.cpp:59, merkle.cpp:27-28)
 #include <cstdint>
 #include <cstring>
 #include <limits>
 #include <random>
 
 #include "../../include/nasp_bloom.h"
+#include "bloom_math.h"
 
 extern "C" {
 
@@ -17,6 +19,18 @@ uint64_t nb_seed_from_time(uint32_t time_const) {
     std::mt19937 rng(time_const);
     std::uniform_int_distribution<uint64_t> dist(0, std::numeric_limits<uint64_t>::max());
     return dist(rng);
+}
+
+uint64_t nb_std_hash(const uint8_t *p, uint64_t len, int flavor) {
+    // the kernels' word-stream hash over byte-assembled words (never reads past len)
+    auto load = [p, len](uint32_t j) {
+        uint64_t w = 0;
+        for (uint64_t b = 0; b < 8 && 8ull * j + b < len; ++b) w |= (uint64_t)p[8ull * j + b] << (8 * b);
+        return w;
+    };
+    return flavor == NB_FLAVOR_MSVC_FNV1A
+               ? nb::hash1_aligned_words<NB_FLAVOR_MSVC_FNV1A>(load, 0, (uint32_t)len)
+               : nb::hash1_aligned_words<NB_FLAVOR_LIBSTDCXX>(load, 0, (uint32_t)len);
 }
 
 size_t nb_serialized_size(uint32_t m) {

@@ -25,7 +25,8 @@
 
 #include <stdint.h>
 
-#if defined(__HIPCC__)
+#if defined(__HIP__)  // compiled as HIP (hipcc); plain C++ (g++) otherwise
+#include <hip/hip_runtime.h>
 #define NB_HD __host__ __device__ __forceinline__
 #else
 #define NB_HD inline
@@ -298,6 +299,103 @@ NB_HD void hash_aligned_words(const FilterConsts &c, LoadQ Q, uint32_t a, uint32
         }
         lsx_end(c, s, len, h1, h2);
     }
+}
+
+// ------------------------------------------------------------- Merkle ----
+// MerkleTree (reference MerkleTree/merkle.cpp:7-55) hashes with the same
+// std::hash<std::string> as the filter, over decimal strings: a leaf is
+// to_string(H(record)), a parent to_string(H(left ++ right)) (merkle.cpp:26-32,48).
+
+// H(bytes) alone (no seed prefix): the filter's h1 (hash_aligned_words' first half).
+template <int FLAVOR, class LoadQ>
+NB_HD uint64_t hash1_aligned_words(LoadQ Q, uint32_t a, uint32_t len) {
+    const uint32_t nq = (a + len + 7) >> 3;
+    const uint32_t nk = (len + 7) >> 3;
+    uint64_t qcur = nq ? Q(0) : 0;
+    uint64_t h = FLAVOR == 1 ? kFnvBasis : lsx_init(len);
+    for (uint32_t j = 0; j < nk; ++j) {
+        const uint64_t qnext = (j + 1 < nq) ? Q(j + 1) : 0;
+        const uint64_t kw = mask_bytes(funnel(qcur, qnext, 8 * a), (int)(len - 8 * j));
+        qcur = qnext;
+        if (FLAVOR == 1) {
+            for (int b = 0; b < 8; ++b)
+                if (b < (int)(len - 8 * j)) h = fnv_step(h, (uint32_t)(kw >> (8 * b)) & 0xffu);
+        } else {
+            h = (j < (len >> 3)) ? lsx_round(h, kw) : lsx_tail(h, kw);
+        }
+    }
+    return FLAVOR == 1 ? h : lsx_final(h);
+}
+
+// Four decimal digits of y < 10^4 as ASCII bytes, most significant first (LE u32).
+NB_HD uint32_t dec4(uint32_t y) {
+    const uint32_t a = y / 100, b = y - a * 100;
+    const uint32_t a1 = a / 10, a0 = a - a1 * 10, b1 = b / 10, b0 = b - b1 * 10;
+    return (a1 | (a0 << 8) | (b1 << 16) | (b0 << 24)) + 0x30303030u;
+}
+// Eight decimal digits of c < 10^8, most significant first (LE u64).
+NB_HD uint64_t dec8(uint32_t c) {
+    const uint32_t hi = c / 10000, lo = c - hi * 10000;
+    return (uint64_t)dec4(hi) | ((uint64_t)dec4(lo) << 32);
+}
+
+// to_string(x) (what `stringstream << size_t` writes, merkle.cpp:29-31): its
+// D = 1..20 ASCII digits left-aligned in w[0..2] (byte i = character i, zero
+// bytes after the last digit).  Returns D.
+NB_HD uint32_t u64_to_dec(uint64_t x, uint64_t w[3]) {
+    const uint64_t q = x / 100000000ull;
+    const uint32_t c0 = (uint32_t)(x - q * 100000000ull);
+    const uint32_t c2 = (uint32_t)(q / 100000000ull);  // < 1845
+    const uint32_t c1 = (uint32_t)(q - (uint64_t)c2 * 100000000ull);
+    const uint64_t d1 = dec8(c1), d0 = dec8(c0);
+    // the 20-character zero-padded string: c2 (4) | c1 (8) | c0 (8)
+    const uint64_t p0 = (uint64_t)dec4(c2) | (d1 << 32);
+    const uint64_t p1 = (d1 >> 32) | (d0 << 32);
+    const uint64_t p2 = d0 >> 32;
+    // leading '0' characters to drop: the first non-'0' byte (the last one kept)
+    const uint64_t z0 = p0 ^ 0x3030303030303030ull, z1 = p1 ^ 0x3030303030303030ull;
+    const uint64_t z2 = (p2 ^ 0x30303030ull) & 0xffffffffull;
+    uint32_t z;
+    if (z0) z = (uint32_t)(__builtin_ctzll(z0) >> 3);
+    else if (z1) z = 8 + (uint32_t)(__builtin_ctzll(z1) >> 3);
+    else if (z2) z = 16 + (uint32_t)(__builtin_ctzll(z2) >> 3);
+    else z = 19;  // x == 0: "0"
+    // shift left by z bytes (selects, not an indexed array: no scratch on the device)
+    const uint32_t zq = z >> 3, zr = 8 * (z & 7);
+    auto pick = [&](uint32_t i) -> uint64_t { return i == 0 ? p0 : i == 1 ? p1 : i == 2 ? p2 : 0; };
+    for (uint32_t j = 0; j < 3; ++j) {
+        const uint64_t lo = pick(j + zq), hi = pick(j + zq + 1);
+        w[j] = zr ? (lo >> zr) | (hi << (64 - zr)) : lo;
+    }
+    return 20 - z;
+}
+
+// H(to_string(l) ++ to_string(r)): a Merkle parent (merkle.cpp:44-48).
+template <int FLAVOR>
+NB_HD uint64_t hash_dec_pair(uint64_t l, uint64_t r) {
+    uint64_t wl[3], wr[3];
+    const uint32_t dl = u64_to_dec(l, wl), dr = u64_to_dec(r, wr);
+    const uint32_t len = dl + dr, q = dl >> 3, s = 8 * (dl & 7);
+    // r's characters shifted to byte offset dl: sr[j] lands in word q + j
+    const uint64_t sr0 = wr[0] << s, sr1 = s ? (wr[1] << s) | (wr[0] >> (64 - s)) : wr[1],
+                   sr2 = s ? (wr[2] << s) | (wr[1] >> (64 - s)) : wr[2],
+                   sr3 = s ? wr[2] >> (64 - s) : 0;
+    auto pick = [&](uint32_t i) -> uint64_t {  // sr[i], zero outside 0..3
+        return i == 0 ? sr0 : i == 1 ? sr1 : i == 2 ? sr2 : i == 3 ? sr3 : 0;
+    };
+    uint64_t S[5];
+    for (uint32_t j = 0; j < 5; ++j) S[j] = (j < 3 ? wl[j] : 0) | (j >= q ? pick(j - q) : 0);
+    uint64_t h = FLAVOR == 1 ? kFnvBasis : lsx_init(len);
+    for (uint32_t j = 0; j < 5; ++j) {
+        if (8 * j >= len) break;
+        if (FLAVOR == 1) {
+            for (uint32_t b = 0; b < 8 && 8 * j + b < len; ++b)
+                h = fnv_step(h, (uint32_t)(S[j] >> (8 * b)) & 0xffu);
+        } else {
+            h = (j < (len >> 3)) ? lsx_round(h, S[j]) : lsx_tail(h, S[j]);
+        }
+    }
+    return FLAVOR == 1 ? h : lsx_final(h);
 }
 
 // -------------------------------------------------------- host reference ----

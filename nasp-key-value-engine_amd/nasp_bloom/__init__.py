@@ -10,9 +10,12 @@ is the Python binding used by tests/ and bench.py:
                                   upload / device build overlapped (nb_builder_*)
   BloomFilter                  -- mirror of the reference class surface
                                   (reference BloomFilter/BloomFilter.h:24-41)
+  MerkleTree, merkle_device    -- the SSTable Merkle tree on the GPU (nb_merkle*), mirror
+                                  of the reference class (MerkleTree/MerkleTree.h:10-36)
   distributed                  -- multi-GPU: independent filters / cooperative OR-merge
 """
 from ._lib import (FLAVOR_LIBSTDCXX, FLAVOR_MSVC_FNV1A, NaspBloomError, lib)  # noqa: F401
-from .api import (BloomFilter, Builder, build_device, build_host, deserialize, nwords, or_merge_device,  # noqa: F401
+from .api import (BloomFilter, Builder, MerkleTree, build_device, merkle_device, merkle_host,  # noqa: F401
+                  merkle_tree_size, std_hash, build_host, deserialize, nwords, or_merge_device,  # noqa: F401
                   probe_device, probe_host, seed_from_time, serialize, size_of_bitset,
                   num_hashes)

@@ -32,6 +32,7 @@ _SIGS = {
     "nb_size_of_bitset": (C.c_uint32, [C.c_uint32, C.c_double]),
     "nb_num_hashes": (C.c_uint32, [C.c_uint32, C.c_uint32]),
     "nb_seed_from_time": (C.c_uint64, [C.c_uint32]),
+    "nb_std_hash": (C.c_uint64, [C.c_void_p, C.c_uint64, C.c_int]),
     "nb_build": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
                            C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_int]),
     "nb_probe": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
@@ -64,6 +65,11 @@ _SIGS = {
                                        C.c_uint64]),
     "nb_builder_finish": (C.c_int, [C.c_void_p, C.c_void_p]),
     "nb_builder_destroy": (C.c_int, [C.c_void_p]),
+    "nb_merkle_tree_size": (C.c_uint64, [C.c_uint64]),
+    "nb_merkle_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_int,
+                                   C.c_void_p, C.c_void_p]),
+    "nb_merkle": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_int, C.c_void_p,
+                            C.c_void_p, C.c_void_p, C.c_int]),
 }
 
 FRAME_RAW = 0

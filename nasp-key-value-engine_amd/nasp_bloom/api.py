@@ -36,6 +36,11 @@ def seed_from_time(time_const: int) -> int:
     return int(lib().nb_seed_from_time(time_const))
 
 
+def std_hash(data: bytes, flavor: int = FLAVOR_LIBSTDCXX) -> int:
+    """std::hash<std::string> of the flavour (host function of the library)."""
+    return int(lib().nb_std_hash(data, len(data), flavor))
+
+
 def _stream_handle(stream) -> int | None:
     if stream is None:
         import torch
@@ -260,3 +265,86 @@ class BloomFilter:
         bf.m, bf.k, bf.p, bf.timeConst, bf.h2_seed = self.m, self.k, self.p, self.timeConst, self.h2_seed
         bf.words = self.words.copy()
         return bf
+
+
+# ------------------------------------------------------------------ Merkle --
+
+def merkle_tree_size(n: int) -> int:
+    return int(lib().nb_merkle_tree_size(n))
+
+
+def merkle_device(data, offsets, rec_len: int, n: int, flavor: int, tree, stream=None) -> None:
+    """Every level of the Merkle tree of n device-resident records into `tree`
+    (merkle_tree_size(n) int64/uint64 cuda words; leaves first, root last)."""
+    if not data.is_cuda or not tree.is_cuda or (offsets is not None and not offsets.is_cuda):
+        raise NaspBloomError("merkle_device needs CUDA (HIP) tensors")
+    if tree.numel() * tree.element_size() < merkle_tree_size(n) * 8:
+        raise NaspBloomError("tree tensor smaller than merkle_tree_size(n) words")
+    check(lib().nb_merkle_device(data.data_ptr(), offsets.data_ptr() if offsets is not None else None,
+                                 rec_len, n, flavor, tree.data_ptr(), _stream_handle(stream)),
+          "nb_merkle_device")
+
+
+def merkle_host(data: np.ndarray, offsets: np.ndarray | None, rec_len: int, n: int,
+                flavor: int = FLAVOR_LIBSTDCXX, device: int = 0, want_tree: bool = True):
+    """-> (root hash, tree words or None).  tree[:n] are the leaves."""
+    tree = np.zeros(merkle_tree_size(n), dtype=np.uint64) if want_tree else None
+    root = C.c_uint64()
+    check(lib().nb_merkle(_np_ptr(data), _np_ptr(offsets), rec_len, n, flavor, _np_ptr(tree), None,
+                          C.addressof(root), device), "nb_merkle")
+    return int(root.value), tree
+
+
+class MerkleTree:
+    """Mirror of the reference MerkleTree (MerkleTree/MerkleTree.h:10-36): the tree is
+    built on the GPU; strings are the decimal hashes the reference stores."""
+
+    def __init__(self, data, *, flavor: int = FLAVOR_LIBSTDCXX, device: int = 0):
+        recs = [d.encode() if isinstance(d, str) else bytes(d) for d in data]
+        if not recs:
+            raise ValueError("Merkle tree of no data (merkle.cpp:8-10 throws)")
+        self.flavor = flavor
+        buf, offs = _pack(recs)
+        self._n = len(recs)
+        _, self._tree = merkle_host(buf, offs, 0, self._n, flavor, device)
+        self._levels = []
+        at, c = 0, self._n
+        while True:
+            self._levels.append((at, c))
+            at += c
+            if c == 1:
+                break
+            c = (c + 1) // 2
+
+    def _hash(self, data: bytes) -> str:  # merkle.cpp:26-32
+        return str(std_hash(data, self.flavor))
+
+    def getRootHash(self) -> str:
+        return str(int(self._tree[-1]))
+
+    def getLeaves(self) -> list[str]:
+        return [str(int(x)) for x in self._tree[: self._n]]
+
+    def generateProof(self, data) -> list[tuple[str, bool]]:  # merkle.cpp:57-84
+        h = std_hash(data.encode() if isinstance(data, str) else bytes(data), self.flavor)
+        hits = np.nonzero(self._tree[: self._n] == np.uint64(h))[0]
+        if hits.size == 0:
+            raise ValueError("record not in the Merkle tree (merkle.cpp:63-65 throws)")
+        index = int(hits[0])
+        proof = []
+        for at, cnt in self._levels[:-1]:
+            is_right = index % 2 == 1
+            sib = index - 1 if is_right else index + 1
+            if sib < cnt:
+                proof.append((str(int(self._tree[at + sib])), is_right))
+            index //= 2
+        return proof
+
+    @staticmethod
+    def verifyProof(rootHash: str, data, proof, flavor: int = FLAVOR_LIBSTDCXX) -> bool:
+        h = lambda s: str(std_hash(s.encode(), flavor))  # noqa: E731
+        d = data.encode() if isinstance(data, str) else bytes(data)
+        computed = str(std_hash(d, flavor))
+        for sib, is_right in proof:  # merkle.cpp:90-99
+            computed = h(sib + computed) if is_right else h(computed + sib)
+        return computed == rootHash

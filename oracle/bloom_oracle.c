@@ -235,3 +235,56 @@ size_t orc_serialize(uint32_t m, uint32_t k, double p, uint32_t time_const,
     memcpy(out + 28, words, nbytes);
     return 28 + nbytes;
 }
+
+/* ---------------------------------------------------------------- Merkle --
+ * merkle.cpp:26-32: hash(data) = stringstream << std::hash<std::string>(data),
+ * i.e. the decimal digits of the size_t hash.  Restated with snprintf. */
+static int dec_of(uint64_t v, char out[24]) {
+    return snprintf(out, 24, "%llu", (unsigned long long)v);
+}
+
+static uint64_t hash_pair(int flavor, uint64_t l, uint64_t r) {
+    char buf[48];
+    int a = dec_of(l, buf);
+    int b = dec_of(r, buf + a);
+    return orc_hash(flavor, (const uint8_t *)buf, (size_t)(a + b));
+}
+
+uint64_t orc_merkle_tree_size(uint64_t n) {
+    uint64_t total = n;
+    while (n > 1) {
+        n = (n + 1) / 2;
+        total += n;
+    }
+    return total;
+}
+
+uint64_t orc_merkle(int flavor, const uint8_t *data, const uint64_t *offsets, uint32_t rec_len,
+                    uint64_t n, uint64_t *leaves, uint64_t *tree) {
+    if (n == 0) return 0;  /* the reference throws std::invalid_argument (merkle.cpp:8-10) */
+    uint64_t *level = (uint64_t *)malloc(n * sizeof(uint64_t));
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint8_t *p = offsets ? data + offsets[i] : data + i * (uint64_t)rec_len;
+        const size_t len = offsets ? (size_t)(offsets[i + 1] - offsets[i]) : rec_len;
+        level[i] = orc_hash(flavor, p, len);
+    }
+    if (leaves) memcpy(leaves, level, n * sizeof(uint64_t));
+    uint64_t at = 0;
+    if (tree) memcpy(tree, level, n * sizeof(uint64_t));
+    at = n;
+    uint64_t cnt = n;
+    while (cnt > 1) {  /* merkle.cpp:41-52 */
+        const uint64_t next = (cnt + 1) / 2;
+        for (uint64_t i = 0; i < next; ++i) {
+            const uint64_t l = level[2 * i];
+            const uint64_t r = (2 * i + 1 < cnt) ? level[2 * i + 1] : l;
+            level[i] = hash_pair(flavor, l, r);
+        }
+        cnt = next;
+        if (tree) memcpy(tree + at, level, cnt * sizeof(uint64_t));
+        at += cnt;
+    }
+    const uint64_t root = level[0];
+    free(level);
+    return root;
+}

@@ -52,6 +52,18 @@ int orc_probe(int flavor, const uint8_t *keys, const uint64_t *offsets,
               uint32_t key_len, uint64_t n, uint32_t m, uint32_t k,
               uint64_t seed, const uint64_t *words, uint8_t *out);
 
+/*
+ * MerkleTree(data) (reference MerkleTree/merkle.cpp:7-55): leaves[i] = H(record i)
+ * (its decimal string is leaf i, merkle.cpp:13-15,26-32); each level pairs nodes
+ * i, i+1 (the last one with itself when the level is odd) into
+ * H(to_string(left) ++ to_string(right)) until one node is left (merkle.cpp:41-52).
+ * tree (optional, orc_merkle_tree_size(n) words): every level, leaves first.
+ * Returns the root hash (getRootHash() is its decimal string).  n >= 1.
+ */
+uint64_t orc_merkle(int flavor, const uint8_t *data, const uint64_t *offsets, uint32_t rec_len,
+                    uint64_t n, uint64_t *leaves, uint64_t *tree);
+uint64_t orc_merkle_tree_size(uint64_t n);
+
 /* Serialized image (BloomFilter.cpp:88-129): 28-byte header + (uint32)(m+7)/8 bytes. */
 size_t orc_serialized_size(uint32_t m);
 size_t orc_serialize(uint32_t m, uint32_t k, double p, uint32_t time_const,

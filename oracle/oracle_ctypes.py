@@ -5,6 +5,7 @@ this module.  The product path (nasp-key-value-engine_amd/) never does.
 
   Oracle  -> oracle/build/liboracle.so  : CPU restatement (bloom_oracle.c)
   RefLib  -> oracle/_ref/libref_bloom.so: the reference BloomFilter.cpp compiled here
+  RefMerkle -> oracle/_ref/libref_merkle.so: the reference MerkleTree/merkle.cpp compiled here
 """
 from __future__ import annotations
 
@@ -17,6 +18,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "build", "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libref_bloom.so")
+REF_MERKLE_SO = os.path.join(HERE, "_ref", "libref_merkle.so")
 
 LIBSTDCXX = 0
 MSVC_FNV1A = 1
@@ -77,6 +79,10 @@ class Oracle:
         lib.orc_serialize.restype = C.c_size_t
         lib.orc_serialize.argtypes = [C.c_uint32, C.c_uint32, C.c_double, C.c_uint32,
                                       C.c_uint64, _u64p, _u8p]
+        lib.orc_merkle.restype = C.c_uint64
+        lib.orc_merkle.argtypes = [C.c_int, _u8p, _u64p, C.c_uint32, C.c_uint64, _u64p, _u64p]
+        lib.orc_merkle_tree_size.restype = C.c_uint64
+        lib.orc_merkle_tree_size.argtypes = [C.c_uint64]
         self.lib = lib
 
     def hash(self, flavor: int, key: bytes) -> int:
@@ -117,6 +123,14 @@ class Oracle:
         out = np.zeros(self.lib.orc_serialized_size(m), dtype=np.uint8)
         n = self.lib.orc_serialize(m, k, p, tc, seed, _ptr(words, _u64p), _ptr(out))
         return out[:n].tobytes()
+
+    def merkle(self, flavor, data_u8, offsets, rec_len, n, want_tree=False):
+        """-> (root hash, leaf hashes[n], every level [tree size] or None)"""
+        leaves = np.zeros(max(n, 1), dtype=np.uint64)
+        tree = np.zeros(self.lib.orc_merkle_tree_size(n), dtype=np.uint64) if want_tree else None
+        root = self.lib.orc_merkle(flavor, _ptr(data_u8), _ptr(offsets, _u64p), rec_len, n,
+                                   _ptr(leaves, _u64p), _ptr(tree, _u64p))
+        return int(root), leaves[:n], tree
 
 
 class RefLib:
@@ -191,3 +205,53 @@ class RefLib:
     def default_contains(self, key: bytes) -> bool:
         a = np.frombuffer(key + b"\0", dtype=np.uint8)
         return bool(self.lib.ref_default_contains(_ptr(a), len(key)))
+
+
+class RefMerkle:
+    """The reference MerkleTree/merkle.cpp compiled here (oracle/_ref)."""
+
+    def __init__(self, path: str = REF_MERKLE_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        lib = C.CDLL(path)
+        lib.ref_merkle.restype = C.c_int
+        lib.ref_merkle.argtypes = [_u8p, _u64p, C.c_uint32, C.c_uint64, C.c_char_p, _u64p]
+        lib.ref_merkle_timed.restype = C.c_double
+        lib.ref_merkle_timed.argtypes = [_u8p, _u64p, C.c_uint32, C.c_uint64, C.c_char_p]
+        lib.ref_merkle_proof.restype = C.c_int
+        lib.ref_merkle_proof.argtypes = [_u8p, _u64p, C.c_uint32, C.c_uint64, C.c_uint64, _u64p,
+                                         _u8p, C.c_int]
+        lib.ref_merkle_verify.restype = C.c_int
+        lib.ref_merkle_verify.argtypes = [C.c_char_p, _u8p, C.c_uint64, _u64p, _u8p, C.c_int]
+        self.lib = lib
+
+    def merkle(self, data_u8, offsets, rec_len, n):
+        """-> (root string, leaf hashes[n])"""
+        root = C.create_string_buffer(64)
+        leaves = np.zeros(max(n, 1), dtype=np.uint64)
+        rc = self.lib.ref_merkle(_ptr(data_u8), _ptr(offsets, _u64p), rec_len, n, root,
+                                 _ptr(leaves, _u64p))
+        if rc != 0:
+            raise ValueError("reference MerkleTree threw")
+        return root.value.decode(), leaves[:n]
+
+    def merkle_timed(self, data_u8, offsets, rec_len, n):
+        root = C.create_string_buffer(64)
+        t = self.lib.ref_merkle_timed(_ptr(data_u8), _ptr(offsets, _u64p), rec_len, n, root)
+        return t, root.value.decode()
+
+    def proof(self, data_u8, offsets, rec_len, n, target):
+        sib = np.zeros(64, dtype=np.uint64)
+        right = np.zeros(64, dtype=np.uint8)
+        np_ = self.lib.ref_merkle_proof(_ptr(data_u8), _ptr(offsets, _u64p), rec_len, n, target,
+                                        _ptr(sib, _u64p), _ptr(right), 64)
+        if np_ < 0:
+            raise ValueError("reference generateProof threw")
+        return [(int(sib[i]), bool(right[i])) for i in range(np_)]
+
+    def verify(self, root: str, rec: bytes, proof) -> bool:
+        a = np.frombuffer(rec + b"\0", dtype=np.uint8)
+        sib = np.array([p[0] for p in proof] or [0], dtype=np.uint64)
+        right = np.array([1 if p[1] else 0 for p in proof] or [0], dtype=np.uint8)
+        return bool(self.lib.ref_merkle_verify(root.encode(), _ptr(a), len(rec), _ptr(sib, _u64p),
+                                               _ptr(right), len(proof)))

@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <string>
 #include <vector>
 #include "../../nasp-key-value-engine_amd/csrc/bloom_math.h"
 extern "C" {
@@ -84,5 +85,53 @@ int main() {
         }
     }
     printf("hash mismatches: %ld\n", hbad);
-    return (bad || hbad) ? 1 : 0;
+
+    // Merkle helpers (MerkleTree/merkle.cpp:26-32,48): to_string(x) of every digit
+    // count, single-string hash at every misalignment, and the parent hash
+    // H(to_string(l) ++ to_string(r)) against the oracle's snprintf restatement.
+    long mbad = 0;
+    std::vector<uint64_t> xs = {0ull, 1ull, 9ull, 10ull, 99ull, 100ull, 12345678ull, 99999999ull,
+                                100000000ull, 10000000000000000ull, 1844674407370955161ull,
+                                9999999999999999999ull, 10000000000000000000ull, ~0ull};
+    for (uint64_t p10 = 1; p10 < 10000000000000000000ull; p10 *= 10) {
+        xs.push_back(p10);
+        xs.push_back(p10 - 1);
+        xs.push_back(p10 + 1);
+    }
+    for (int t = 0; t < 20000; ++t) xs.push_back(rng() >> (rng() % 64));
+    for (uint64_t x : xs) {
+        uint64_t w[3];
+        const uint32_t d = nb::u64_to_dec(x, w);
+        char want[32];
+        const int wl = snprintf(want, sizeof want, "%llu", (unsigned long long)x);
+        char got[25] = {0};
+        for (int b = 0; b < 24; ++b) got[b] = (char)(w[b / 8] >> (8 * (b % 8)));
+        if ((int)d != wl || std::string(got, d) != std::string(want, wl)) ++mbad;
+        for (int b = d; b < 24; ++b)
+            if (got[b]) { ++mbad; break; }  // zero bytes after the digits
+    }
+    for (int fl = 0; fl < 2; ++fl) {
+        for (int t = 0; t < 20000; ++t) {
+            const uint64_t l = xs[rng() % xs.size()], r = xs[rng() % xs.size()];
+            char buf[48];
+            const int n = snprintf(buf, sizeof buf, "%llu%llu", (unsigned long long)l,
+                                   (unsigned long long)r);
+            const uint64_t want = orc_hash(fl, reinterpret_cast<const uint8_t *>(buf), (size_t)n);
+            const uint64_t got = fl ? nb::hash_dec_pair<1>(l, r) : nb::hash_dec_pair<0>(l, r);
+            if (got != want) ++mbad;
+        }
+        for (int t = 0; t < 3000; ++t) {
+            const size_t len = rng() % 100;
+            alignas(8) uint8_t arena[128 + 16];
+            const uint32_t a = (uint32_t)(rng() % 8);
+            for (size_t b = 0; b < sizeof arena; ++b) arena[b] = (uint8_t)rng();
+            const uint64_t *q = reinterpret_cast<const uint64_t *>(arena + 8);
+            auto load = [q](uint32_t j) { return q[j]; };
+            const uint64_t got = fl ? nb::hash1_aligned_words<1>(load, a, (uint32_t)len)
+                                    : nb::hash1_aligned_words<0>(load, a, (uint32_t)len);
+            if (got != orc_hash(fl, arena + 8 + a, len)) ++mbad;
+        }
+    }
+    printf("merkle mismatches: %ld\n", mbad);
+    return (bad || hbad || mbad) ? 1 : 0;
 }

@@ -1,0 +1,127 @@
+// Drop-in MerkleTree test: drives nasp-key-value-engine_amd/host/MerkleTree the way
+// the reference's callers do and checks every string against the oracle
+// (oracle/bloom_oracle.c orc_merkle).  Needs a GPU (the tree is built on it).
+//   1. the reference's test program (MerkleTree/main.cpp): four records, a proof
+//      for "Podatak2" that verifies;
+//   2. SSTable::build (SSTable/SSTable.cpp:29-42): one value per record, root and
+//      leaves; SSTableRaw's key ++ value records (SSTableRaw.cpp:238);
+//   3. records with NUL bytes and empty records; errors the reference throws.
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../nasp-key-value-engine_amd/host/MerkleTree.h"
+extern "C" {
+#include "../../oracle/bloom_oracle.h"
+}
+
+static int failures = 0;
+#define EXPECT(cond, msg)                                       \
+    do {                                                        \
+        if (!(cond)) {                                          \
+            std::printf("FAIL: %s (line %d)\n", msg, __LINE__); \
+            ++failures;                                         \
+        }                                                       \
+    } while (0)
+
+struct OracleTree {
+    std::string root;
+    std::vector<std::string> leaves;
+};
+
+static OracleTree oracle_tree(const std::vector<std::string> &recs) {
+    std::vector<uint64_t> offs(recs.size() + 1, 0);
+    std::string flat;
+    for (size_t i = 0; i < recs.size(); ++i) {
+        flat += recs[i];
+        offs[i + 1] = flat.size();
+    }
+    flat.append(16, '\0');
+    std::vector<uint64_t> leaves(recs.size());
+    const uint64_t root = orc_merkle(ORC_FLAVOR_LIBSTDCXX, reinterpret_cast<const uint8_t *>(flat.data()),
+                                     offs.data(), 0, recs.size(), leaves.data(), nullptr);
+    OracleTree t;
+    t.root = std::to_string(root);
+    for (uint64_t l : leaves) t.leaves.push_back(std::to_string(l));
+    return t;
+}
+
+// verifyProof (merkle.cpp:86-102) skips a level where the node has no sibling,
+// but buildTree hashed that node with itself: the reference's proofs verify only
+// for records whose path never crosses the last node of an odd level.
+static bool reference_verifies(size_t index, size_t n) {
+    for (size_t c = n; c > 1; c = (c + 1) / 2, index /= 2)
+        if (c % 2 == 1 && index == c - 1) return false;
+    return true;
+}
+
+static void check_tree(const std::vector<std::string> &recs, const char *what) {
+    MerkleTree tree(recs);
+    const OracleTree want = oracle_tree(recs);
+    EXPECT(tree.getRootHash() == want.root, what);
+    EXPECT(tree.getLeaves() == want.leaves, what);
+    for (size_t i = 0; i < recs.size(); i += recs.size() / 7 + 1) {
+        const auto proof = tree.generateProof(recs[i]);
+        size_t first = 0;  // generateProof follows the first equal record
+        while (recs[first] != recs[i]) ++first;
+        EXPECT(MerkleTree::verifyProof(tree.getRootHash(), recs[i], proof) ==
+                   reference_verifies(first, recs.size()),
+               what);
+        EXPECT(!MerkleTree::verifyProof(tree.getRootHash(), recs[i] + "x", proof), what);
+    }
+}
+
+int main() {
+    // 1. MerkleTree/main.cpp
+    {
+        std::vector<std::string> data = {"Podatak1", "Podatak2", "Podatak3", "Podatak4"};
+        MerkleTree tree(data);
+        const auto proof = tree.generateProof("Podatak2");
+        EXPECT(MerkleTree::verifyProof(tree.getRootHash(), "Podatak2", proof), "main.cpp proof");
+        EXPECT(tree.getRootHash() == oracle_tree(data).root, "main.cpp root");
+        EXPECT(proof.size() == 2 && proof[0].second, "main.cpp proof shape");
+    }
+    // 2. SSTable::build values and SSTableRaw key ++ value records
+    {
+        std::vector<std::string> values, kv;
+        char k[32], v[32];
+        for (int i = 0; i < 3001; ++i) {
+            std::snprintf(k, sizeof k, "user%012d", i);
+            std::snprintf(v, sizeof v, "value-%d", i);
+            values.push_back(v);
+            kv.push_back(std::string(k) + v);
+        }
+        check_tree(values, "SSTable::build values");
+        check_tree(kv, "SSTableRaw key+value records");
+        check_tree(std::vector<std::string>(values.begin(), values.begin() + 1), "one record");
+        check_tree(std::vector<std::string>(values.begin(), values.begin() + 3), "three records");
+    }
+    // 3. binary and empty records; errors
+    {
+        std::vector<std::string> recs = {std::string("a\0b", 3), "", std::string(70, '\0'), "z", ""};
+        check_tree(recs, "binary / empty records");
+        bool threw = false;
+        try {
+            MerkleTree none(std::vector<std::string>{});
+        } catch (const std::invalid_argument &) {
+            threw = true;
+        }
+        EXPECT(threw, "empty data throws invalid_argument (merkle.cpp:8-10)");
+        threw = false;
+        try {
+            MerkleTree t(recs);
+            t.generateProof("not-there");
+        } catch (const std::invalid_argument &) {
+            threw = true;
+        }
+        EXPECT(threw, "missing record throws invalid_argument (merkle.cpp:63-65)");
+    }
+    if (failures) {
+        std::printf("%d failures\n", failures);
+        return 1;
+    }
+    std::printf("merkle drop-in OK\n");
+    return 0;
+}

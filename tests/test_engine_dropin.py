@@ -120,9 +120,11 @@ def test_reference_engine_tiered_compaction(tmp_path, oracle, mode, built):
 @pytest.mark.parametrize("mode", ["raw", "comp"])
 @pytest.mark.parametrize("tiered", [False, True])
 def test_engine_with_dropin_on_gpu(tmp_path, oracle, mode, tiered, built):
-    """The reference engine linked against the drop-in class: flush and size-tiered
-    compaction write filters bit-exact with the oracle, framed exactly as the
-    reference frames them, and with the same file set as the reference engine."""
+    """The reference engine linked against the drop-in classes (BloomFilter and
+    MerkleTree): flush and size-tiered compaction write filters bit-exact with the
+    oracle, framed exactly as the reference frames them, the same file set as the
+    reference engine, and every other file -- the meta files with the Merkle root
+    and leaves included -- byte for byte the reference engine's."""
     if not os.path.exists(DROPIN_ENGINE):
         pytest.skip("engine_dropin not built (needs /root/reference at build time)")
     import torch
@@ -147,3 +149,12 @@ def test_engine_with_dropin_on_gpu(tmp_path, oracle, mode, tiered, built):
         assert rel(filter_files(d_ref), d_ref) == rel(files, d_new)
         for f in filter_files(d_ref):
             assert os.path.getsize(f) == os.path.getsize(d_new / os.path.relpath(f, d_ref))
+        # every other file byte for byte: data / index / summary, and the meta files
+        # holding the Merkle root and leaves the drop-in MerkleTree computed on the GPU
+        others = lambda d: sorted(os.path.relpath(os.path.join(r, f), d) for r, _, fs in os.walk(d)
+                                  for f in fs if not re.match(r"filter_(raw|comp)_\d+\.db$", f))
+        assert others(d_ref) == others(d_new)
+        metas = [f for f in others(d_ref) if os.path.basename(f).startswith("meta_")]
+        assert metas, others(d_ref)
+        for f in others(d_ref):
+            assert open(d_ref / f, "rb").read() == open(d_new / f, "rb").read(), f
