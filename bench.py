@@ -150,9 +150,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"],
+    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "merkle"],
                     help="c1-c4: an independent filter per GPU (weak scaling); c5: one "
-                         "cooperative filter over all GPUs (strong scaling, RCCL OR-merge)")
+                         "cooperative filter over all GPUs (strong scaling, RCCL OR-merge); "
+                         "merkle: the SSTable Merkle tree of C2's 10M x 16 B records per GPU")
     ap.add_argument("--flavor", type=int, default=0, help="0 libstdc++ (default), 1 MSVC FNV-1a")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true",
@@ -174,6 +175,8 @@ def main():
     dev = torch.device("cuda", local)
     nbm.lib()  # fail loudly if the HIP library is missing
 
+    if args.workload == "merkle":
+        return bench_merkle(args, world, rank, dev)
     wl = synth.WORKLOADS[args.workload]
     if args.workload == "c5":
         return bench_cooperative(args, wl, world, rank, dev)
@@ -254,6 +257,86 @@ def main():
         out["host_path"] = host_path_rate(wl, keys_np, offs_np, key_len, seed, args.flavor)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(wl, keys_np, offs_np, key_len, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_merkle(args, world, rank, dev):
+    """The Merkle tree SSTable::build makes on the same flush (SSTable.cpp:29-40):
+    every level of the tree of C2's 10M x 16-byte records, device-resident, one
+    independent tree per rank (weak scaling).  Algorithmic bytes: records read once,
+    every node written once and every non-root node read once by its parent."""
+    import torch
+    import torch.distributed as dist
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    wl = synth.C2
+    keys_np, _, kl = synth.keys_for(wl, seed=synth.SEED + rank)
+    data = torch.from_numpy(keys_np).to(dev)
+    tsize = nbm.merkle_tree_size(wl.n)
+    tree = torch.empty(tsize, dtype=torch.int64, device=dev)
+    stream = torch.cuda.Stream(device=dev)
+
+    def step():
+        with torch.cuda.stream(stream):
+            nbm.merkle_device(data, None, kl, wl.n, 0, tree, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from oracle_ctypes import Oracle
+    root, _, _ = Oracle().merkle(0, keys_np, None, kl, wl.n)
+    if int(tree[-1].item()) & 0xFFFFFFFFFFFFFFFF != root:
+        raise SystemExit("Merkle root differs from the oracle -- refusing to report")
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+    B = wl.n * kl + 8 * tsize + 8 * (tsize - 1)
+    achieved = B / (kern_ms * 1e-3) / 1e9
+    out = {"metric": "Merkle tree build Mrecords/s (device-resident), 1/2/4/8 GPU",
+           "value": round(wl.n * args.steps * world / elapsed / 1e6, 3), "unit": "Mrecords/s",
+           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(elapsed / args.steps * 1e3, 5), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+           "data": "synthetic (splitmix64 records, seed 0x5EED+rank)",
+           "config": {"workload": "merkle_c2_10M_x16B", "records_per_gpu": wl.n, "record_bytes": kl,
+                      "tree_nodes": tsize, "parallelism": f"independent tree per GPU x{world}"},
+           "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                        "kernel": "merkle_leaf_kernel + merkle_level_kernel (one tree)",
+                        "kernel_ms": round(kern_ms, 5), "algorithmic_bytes_per_launch": B}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            from oracle_ctypes import RefMerkle
+            ref = RefMerkle()
+            n_cal = 200_000
+            t_cal, _ = ref.merkle_timed(keys_np, None, kl, n_cal)
+            n_s = int(min(wl.n, max(n_cal, n_cal * args.cpu_budget / max(t_cal, 1e-9))))
+            t_s, _ = ref.merkle_timed(keys_np, None, kl, n_s)
+            out["cpu_baseline"] = {"value": round(n_s / t_s / 1e6, 4), "unit": "Mrecords/s",
+                                   "cores": 1, "kind": "reference",
+                                   "sample": f"first {n_s} records: reference MerkleTree(data) "
+                                             f"constructor, {t_s:.1f} s, 1 thread"}
+        except FileNotFoundError:
+            pass
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
