@@ -238,7 +238,7 @@ struct TileCfg {
 constexpr int kBinThreads = 1024;
 constexpr int kBinKPT = 2;       // keys per thread when k <= 8 (1 for larger k)
 constexpr int kTileThreads = 1024;
-constexpr int kTileUnroll = 2;   // 16-byte bucket loads in flight per lane
+constexpr int kTileUnroll = 4;   // 16-byte bucket loads in flight per lane
 constexpr int kShards = 8;
 constexpr uint32_t kStageBytes = 48 * 1024;  // LDS staging window for variable-length keys
 constexpr uint32_t kMaxTiles = 4096;
@@ -734,8 +734,9 @@ __global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
     // the G shards as one flat range of 16-byte vectors
     const ENTRY *tile_base = buckets + (size_t)t * tc.G * tc.cap;
     const uint32_t nvec = shard_v0[tc.G];
+    // a lane's vector indices only grow, so its shard index is advanced, never searched
+    uint32_t g = 0;
     auto vec_at = [&](uint32_t v) {
-        uint32_t g = 0;
         while (g + 1 < tc.G && v >= shard_v0[g + 1]) ++g;
         const uint4 *ev = reinterpret_cast<const uint4 *>(tile_base + (size_t)g * tc.cap);
         return ev[v - shard_v0[g]];

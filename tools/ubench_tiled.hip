@@ -180,6 +180,10 @@ int main(int argc, char **argv) {
                time_bin<kBinKPT, uint16_t, 8>(keys, n, c, tc, sc, buckets, 3),
                time_bin<kBinKPT, uint16_t, 8>(keys, n, c, tc, sc, buckets, 0));
         printf("tile kernel: %.4f ms\n", time_tile<uint16_t, kTileUnroll>(keys, n, c, tc, sc, buckets, words));
+        printf("tile kernel unroll 1/4/8: %.4f %.4f %.4f ms\n",
+               time_tile<uint16_t, 1>(keys, n, c, tc, sc, buckets, words),
+               time_tile<uint16_t, 4>(keys, n, c, tc, sc, buckets, words),
+               time_tile<uint16_t, 8>(keys, n, c, tc, sc, buckets, words));
         // desynchronise the two resident blocks per CU: blocks [lo, 2lo) start late
         for (int lo : {256, 512})
             for (int cyc : {4000, 8000, 16000, 24000}) {
