@@ -251,6 +251,9 @@ constexpr uint32_t kMaxTiles = 4096;
 #ifndef NB_DIAG_PROLOGUE
 #define NB_DIAG_PROLOGUE()
 #endif
+#ifndef NB_TWO_TILE  // diagnostic builds may switch the two-tiles-per-thread tail off
+#define NB_TWO_TILE 1
+#endif
 #ifndef NB_DIAG_NOCOUNT
 #define NB_DIAG_NOCOUNT false
 #endif
@@ -361,8 +364,13 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     const uint32_t total = wave_sums[kWaves];
     const uint32_t shard = blockIdx.x % tc.G;
     uint32_t *cur = sc.gcur + (size_t)shard * T;
-    const uint32_t g0 = h0 ? atomicAdd(&cur[t0], h0) : 0u;
-    const uint32_t g1 = h1 ? atomicAdd(&cur[t0 + 1], h1) : 0u;
+    // reservations on tiles tid and tid + NT: a wave's atomics then hit 64
+    // consecutive cursors (4 lines) instead of 128 at stride 2 -- each device-scope
+    // atomic line is a memory-side request (WRITE_SIZE measured 57 vs 30 MB/build)
+    const uint32_t ta = tid, tb = tid + NT;
+    const uint32_t ha = ta < T ? cnt[ta] : 0u, hb = tb < T ? cnt[tb] : 0u;
+    const uint32_t ga = ha ? atomicAdd(&cur[ta], ha) : 0u;
+    const uint32_t gb = hb ? atomicAdd(&cur[tb], hb) : 0u;
     if (t0 < T) S4[t0] = sort_b + 4 * st0;  // (S4 + t0 is 8-byte aligned only for even T)
     if (t0 + 1 < T) S4[t0 + 1] = sort_b + 4 * st1;
     __syncthreads();
@@ -378,19 +386,24 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
                         ridx[p][j];
         }
     }
-    const int ovf = ((uint64_t)g0 + h0 > tc.cap) | ((uint64_t)g1 + h1 > tc.cap);
+    const int ovf = ((uint64_t)ga + ha > tc.cap) | ((uint64_t)gb + hb > tc.cap);
     const bool any_ovf = __syncthreads_or(ovf) != 0;  // cnt and S4 are dead now
     // run table: first-entry index minus the run's local start (wrapping u32), in
     // bytes when the buckets fit 32-bit offsets; limits over S4 on overflow
     const bool b32 = (uint64_t)T * tc.G * tc.cap * sizeof(ENTRY) <= 0xFFFFFFFFull;
     const uint32_t esz = (b32 && !any_ovf) ? (uint32_t)sizeof(ENTRY) : 1u;
-    if (t0 < T) {
-        cnt[t0] = ((t0 * tc.G + shard) * tc.cap + g0 - st0) * esz;
-        if (any_ovf) S4[t0] = st0 + (g0 < tc.cap ? tc.cap - g0 : 0u);
-    }
-    if (t0 + 1 < T) {
-        cnt[t0 + 1] = (((t0 + 1) * tc.G + shard) * tc.cap + g1 - st1) * esz;
-        if (any_ovf) S4[t0 + 1] = st1 + (g1 < tc.cap ? tc.cap - g1 : 0u);
+    auto run_entry = [&](uint32_t t, uint32_t g) {
+        const uint32_t st = (S4[t] - sort_b) / 4;
+        cnt[t] = ((t * tc.G + shard) * tc.cap + g - st) * esz;
+        return st;
+    };
+    uint32_t sa = 0, sbb = 0;
+    if (ta < T) sa = run_entry(ta, ga);
+    if (tb < T) sbb = run_entry(tb, gb);
+    if (any_ovf) {
+        __syncthreads();  // every thread has read S4 before limits go over it
+        if (ta < T) S4[ta] = sa + (ga < tc.cap ? tc.cap - ga : 0u);
+        if (tb < T) S4[tb] = sbb + (gb < tc.cap ? tc.cap - gb : 0u);
     }
     __syncthreads();
     if (NB_DIAG_STOP(3)) return;
@@ -541,7 +554,7 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     }
     __syncthreads();
     if (NB_DIAG_STOP(1)) return;
-    if (KR > 0 && T <= 2 * NT) {  // block-uniform: the common case (e.g. C2's 1 463 tiles)
+    if (NB_TWO_TILE && KR > 0 && T <= 2 * NT) {  // block-uniform: the common case (C2: T = 1 463)
         bin_tail_two_tiles<NT, KPT, kR>(lds, bin_sort_offset_words(T), tc, sc, buckets, base, n,
                                         c.k, ridx, rank);
         return;
