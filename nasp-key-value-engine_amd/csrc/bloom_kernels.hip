@@ -251,6 +251,9 @@ constexpr uint32_t kMaxTiles = 4096;
 #ifndef NB_DIAG_PROLOGUE
 #define NB_DIAG_PROLOGUE()
 #endif
+#ifndef NB_DIAG_WO  // diagnostic write-out variants: 1 = LDS reads only, 2 = no run lookup
+#define NB_DIAG_WO 0
+#endif
 #ifndef NB_TWO_TILE  // diagnostic builds may switch the two-tiles-per-thread tail off
 #define NB_TWO_TILE 1
 #endif
@@ -418,7 +421,11 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
 #pragma unroll
             for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) g[u] = GX[v[u] >> tc.ts];
+            for (int u = 0; u < 4; ++u) g[u] = NB_DIAG_WO == 2 ? 0u : GX[v[u] >> tc.ts];
+            if (NB_DIAG_WO == 1) {  // diagnostic: LDS reads only
+                if ((v[0] ^ v[1] ^ v[2] ^ v[3] ^ g[0] ^ g[1] ^ g[2] ^ g[3]) == 0xFFFFFFFFu) bb[0] = 1;
+                continue;
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u)
                 *reinterpret_cast<ENTRY *>(bb + (g[u] + (j + u * NT) * (uint32_t)sizeof(ENTRY))) =
