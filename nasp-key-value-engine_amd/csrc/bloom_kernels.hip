@@ -514,46 +514,48 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
             }
         }
     } else {
-        // Variable-length (or odd fixed-length) keys: the block's keys are one
-        // contiguous byte range.  When it fits the stage (the not-yet-used sort
-        // array) it is loaded into LDS with coalesced 16-byte loads and every key
-        // is hashed from LDS; otherwise (very long keys) the lanes read HBM.
+        // Variable-length (or odd fixed-length) keys, one sub-batch of NT keys at a
+        // time: its keys are one contiguous byte range.  When that fits the stage
+        // (the not-yet-used sort array) it is loaded into LDS with coalesced 16-byte
+        // loads and every key is hashed from LDS; otherwise (very long keys) the
+        // lanes read HBM.
         uint8_t *stage = reinterpret_cast<uint8_t *>(sorted);
-        const uint64_t blk_end = min(base + (uint64_t)KPT * NT, n);
         auto koff = [&](uint64_t i) -> uint64_t {
             return LAYOUT == kOffsets ? offsets[i] : i * (uint64_t)key_len;
         };
-        uint64_t b[KPT], e[KPT];
 #pragma unroll
         for (int p = 0; p < KPT; ++p) {
-            const uint64_t i = base + (uint64_t)p * NT + tid;
-            b[p] = e[p] = 0;
-            if (i < n) { b[p] = koff(i); e[p] = koff(i + 1); }
-        }
-        const uint64_t wb = koff(base) & ~15ull;
-        const uint64_t span = koff(blk_end) - wb;
-        const bool staged = span <= (uint64_t)kStageBytes;  // block-uniform
-        if (staged) {
-            const uint4 *src = reinterpret_cast<const uint4 *>(keys + wb);
-            uint4 *dst = reinterpret_cast<uint4 *>(stage);
-            const uint32_t nvec = (uint32_t)((span + 15) / 16);
-            for (uint32_t q = tid; q < nvec; q += NT) dst[q] = src[q];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int p = 0; p < KPT; ++p) {
-            const uint64_t i = base + (uint64_t)p * NT + tid;
+            const uint64_t pb = base + (uint64_t)p * NT;  // first key of the sub-batch
+            if (pb >= n) break;                           // block-uniform
+            const uint64_t pe = min(pb + NT, n);
+            const uint64_t i = pb + tid;
+            uint64_t b = 0, e = 0;
+            if (i < n) {
+                b = koff(i);
+                e = koff(i + 1);
+            }
+            const uint64_t wb = koff(pb) & ~15ull;
+            const uint64_t span = koff(pe) - wb;
+            const bool staged = span <= (uint64_t)kStageBytes;  // block-uniform
+            if (p) __syncthreads();  // the previous sub-batch is hashed: the stage is free
+            if (staged) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(keys + wb);
+                uint4 *dst = reinterpret_cast<uint4 *>(stage);
+                const uint32_t nvec = (uint32_t)((span + 15) / 16);
+                for (uint32_t q = tid; q < nvec; q += NT) dst[q] = src[q];
+            }
+            __syncthreads();
             if (i < n) {
                 uint64_t h1, h2;
-                const uint32_t len = (uint32_t)(e[p] - b[p]);
+                const uint32_t len = (uint32_t)(e - b);
                 if (staged) {
-                    const uint32_t lo = (uint32_t)(b[p] - wb), a = lo & 7u;
+                    const uint32_t lo = (uint32_t)(b - wb), a = lo & 7u;
                     const uint64_t *q = reinterpret_cast<const uint64_t *>(stage + (lo - a));
                     auto load = [q](uint32_t j) { return q[j]; };
                     nb::hash_aligned_words<FLAVOR, decltype(load), LAYOUT == kFixedStride>(
                         c, load, a, len, &h1, &h2);
                 } else {
-                    key_hashes_ptr<FLAVOR, LAYOUT == kFixedStride>(c, keys + b[p], len, &h1, &h2);
+                    key_hashes_ptr<FLAVOR, LAYOUT == kFixedStride>(c, keys + b, len, &h1, &h2);
                 }
                 count_key(p, h1, h2);
             }
@@ -1041,7 +1043,10 @@ int launch_build_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
                     keys, offsets, key_len, n, c, words, overwrite, st);
             return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, false, 0>(
                 keys, offsets, key_len, n, c, words, overwrite, st);
-        } else {  // variable-length / odd-stride keys: LDS-staged reads
+        } else {  // variable-length / odd-stride keys: LDS-staged reads, NT keys at a time
+            if (c.k <= 8 && rank)
+                return launch_tiled<FLAVOR, LAYOUT, kBinKPT, kBinThreads, true, 8>(
+                    keys, offsets, key_len, n, c, words, overwrite, st);
             if (c.k <= 16 && rank)
                 return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, true, 16>(
                     keys, offsets, key_len, n, c, words, overwrite, st);
