@@ -123,6 +123,38 @@ def host_path_rate(wl, keys_np, offs_np, key_len, seed, flavor, reps=3):
     return out
 
 
+def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=5):
+    """Batch possiblyContains (nb_probe_device, BloomFilter.cpp:67-80) over the filter
+    just built: the batch's own keys (every one present: k gathers each) and as many
+    absent keys (early exit at the first zero bit; their positive rate is the
+    filter's measured false-positive rate).  Reported beside `value`."""
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    a_np, a_offs, _ = synth.keys_for(wl, seed=synth.SEED + 1000)
+    absent = torch.from_numpy(a_np).to(dev)
+    a_o = torch.from_numpy(a_offs.view(np.int64)).to(dev) if a_offs is not None else None
+    out_t = torch.empty(wl.n, dtype=torch.uint8, device=dev)
+    res = {}
+    for name, kk, oo in (("present", keys, offs), ("absent", absent, a_o)):
+        with torch.cuda.stream(stream):
+            nbm.probe_device(kk, oo, key_len, wl.n, wl.m, wl.k, seed, flavor, words, out_t,
+                             stream=stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            with torch.cuda.stream(stream):
+                nbm.probe_device(kk, oo, key_len, wl.n, wl.m, wl.k, seed, flavor, words, out_t,
+                                 stream=stream)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        ms = e0.elapsed_time(e1) / reps
+        res[name] = {"value": round(wl.n / (ms * 1e-3) / 1e6, 3), "unit": "Mkeys/s", "ms": round(ms, 4),
+                     "positive_rate": round(float(out_t.float().mean()), 6)}
+    res["note"] = "one lane per key, k gathers with early exit; absent keys from another seed"
+    return res
+
+
 def latest_traffic(workload_name):
     """Per-launch HBM bytes of the build kernel from the committed PMC summary
     (profiles/*pmc*.json, written by tools/pmc_traffic.py), or None."""
@@ -158,6 +190,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the host-buffer (H2D + build + D2H) rate measurement")
+    ap.add_argument("--no-probe", action="store_true", help="skip the batch-probe rates")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
 
@@ -253,6 +286,8 @@ def main():
                       "flavor": ["libstdc++", "msvc-fnv1a"][args.flavor],
                       "parallelism": f"independent filter per GPU x{world}"},
            "roofline": roofline}
+    if rank == 0 and world == 1 and not args.no_probe:
+        out["probe"] = probe_rates(wl, keys, offs, key_len, seed, args.flavor, words, stream, dev)
     if rank == 0 and world == 1 and not args.no_host_path:
         out["host_path"] = host_path_rate(wl, keys_np, offs_np, key_len, seed, args.flavor)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
