@@ -233,6 +233,9 @@ struct TileCfg {
     uint32_t T;      // number of tiles = ceil(m / 2^ts)
     uint32_t G;      // cursor/bucket shards per tile
     uint32_t cap;    // capacity (entries) of one (tile, shard) bucket, multiple of 8
+    uint32_t fts;    // log2 bits of the tiles the spill flags index: ts, except in
+                     // pass 1 of the two-level build (super tiles), where it is the
+                     // fine tiles' ts
 };
 
 constexpr int kBinThreads = 1024;
@@ -435,17 +438,31 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
             const uint32_t v = sorted[j];
             *reinterpret_cast<ENTRY *>(bb + (GX[v >> tc.ts] + j * (uint32_t)sizeof(ENTRY))) = (ENTRY)v;
         }
+    } else if (!any_ovf) {  // buckets past 4 GiB: entry indices, 64-bit addresses
+        uint32_t j = tid;
+        for (; j + 3 * NT < total; j += 4 * NT) {
+            uint32_t v[4], g[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) g[u] = GX[v[u] >> tc.ts];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) buckets[(uint32_t)(g[u] + j + u * NT)] = (ENTRY)v[u];
+        }
+        for (; j < total; j += NT) {
+            const uint32_t v = sorted[j];
+            buckets[(uint32_t)(GX[v >> tc.ts] + j)] = (ENTRY)v;
+        }
     } else {
-        // 64-bit entry addresses; on overflow entries past a bucket's capacity go
-        // to the spill bitmap
+        // overflow: entries past a bucket's capacity go to the spill bitmap
         for (uint32_t j = tid; j < total; j += NT) {
             const uint32_t v = sorted[j], t = v >> tc.ts;
-            if (!any_ovf || j < S4[t]) {
+            if (j < S4[t]) {
                 buckets[(uint32_t)(GX[t] + j)] = (ENTRY)v;
             } else {
                 __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT);
-                sc.spill_flag[t] = 1u;
+                sc.spill_flag[v >> tc.fts] = 1u;
             }
         }
     }
@@ -694,7 +711,7 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
         } else {
             __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
                                   __HIP_MEMORY_SCOPE_AGENT);
-            sc.spill_flag[v >> tc.ts] = 1u;
+            sc.spill_flag[v >> tc.fts] = 1u;
         }
     };
     uint32_t j = tid;
@@ -711,6 +728,89 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     for (; j < total; j += NT) {
         const uint32_t v = sorted[j];
         emit(j, v, GL[v >> tc.ts]);
+    }
+}
+
+// Two-level build for very large filters (T > 2 NT fine tiles, e.g. C5's 4 096
+// tiles of 2^20 bits): binned straight into fine tiles, a block's 1 024 keys x k
+// indices spread over T tiles make runs of ~2.5 entries -- every run a separate
+// reservation atomic and L2 write request.  Pass 1 (the bin kernel with 2^(ts+6)-bit
+// super tiles, full 32-bit indices) makes runs of ~k x 1 024 / T1; pass 2 (this
+// kernel) re-bins each super tile's entries into its 64 fine tiles by an LDS
+// counting sort over 16 384 entries per block (runs of ~256); pass 3 is the tile
+// kernel on the fine tiles.  One extra read + write of the entries buys runs two
+// orders of magnitude longer.  grid = (blocks per super tile, super tiles).
+constexpr uint32_t kSuperFine = 64;  // fine tiles per super tile
+constexpr uint32_t kMaxSuper = 64;   // super tiles (m < 2^32 with 2^26-bit super tiles)
+constexpr int kRebinThreads = 1024;
+constexpr int kRebinEPT = 16;        // entries per thread
+constexpr uint32_t kRebinSpan = kRebinThreads * kRebinEPT;
+
+__global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
+    TileCfg t1, TileCfg t2, TileScratch sc1, TileScratch sc2, const uint32_t *__restrict__ b1,
+    uint32_t *__restrict__ b2) {
+    __shared__ uint32_t v0[kShards + 1];
+    __shared__ uint32_t fcnt[kSuperFine], fS[kSuperFine], fGX[kSuperFine], flim[kSuperFine];
+    __shared__ int any_ovf;
+    extern __shared__ uint32_t sorted[];  // [kRebinSpan]
+    const uint32_t tid = threadIdx.x, s = blockIdx.y;
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (uint32_t g = 0; g < t1.G; ++g) {
+            v0[g] = acc;
+            acc += min(sc1.gcur[(size_t)g * t1.T + s], t1.cap);
+        }
+        v0[t1.G] = acc;
+        any_ovf = 0;
+    }
+    if (tid < kSuperFine) fcnt[tid] = 0;
+    __syncthreads();
+    const uint32_t total = v0[t1.G];
+    const uint32_t first = blockIdx.x * kRebinSpan;
+    if (first >= total) return;  // block-uniform
+    const uint32_t cnt = min(kRebinSpan, total - first);
+    const uint32_t fbase = s * kSuperFine;  // first fine tile of super tile s
+    // load this block's entries (the G shards as one flat range), count per fine tile
+    uint32_t v[kRebinEPT], r[kRebinEPT];
+    uint32_t g = 0;
+#pragma unroll
+    for (int u = 0; u < kRebinEPT; ++u) {
+        const uint32_t q = first + tid + u * kRebinThreads;
+        if (q < first + cnt) {
+            while (g + 1 < t1.G && q >= v0[g + 1]) ++g;
+            v[u] = b1[(size_t)(s * t1.G + g) * t1.cap + (q - v0[g])];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < kRebinEPT; ++u)
+        if (tid + u * kRebinThreads < cnt) r[u] = atomicAdd(&fcnt[(v[u] >> t2.ts) - fbase], 1u);
+    __syncthreads();
+    if (tid < kSuperFine) {  // wave 0: scan the 64 counts, reserve the 64 runs
+        const uint32_t c = fcnt[tid];
+        const uint32_t st = wave_inclusive_scan(c) - c;
+        const uint32_t t = fbase + tid;
+        const uint32_t shard = (blockIdx.y * gridDim.x + blockIdx.x) % t2.G;
+        const uint32_t gr = c ? atomicAdd(&sc2.gcur[(size_t)shard * t2.T + t], c) : 0u;
+        fS[tid] = st;
+        fGX[tid] = (t * t2.G + shard) * t2.cap + gr - st;
+        flim[tid] = st + (gr < t2.cap ? t2.cap - gr : 0u);
+        if ((uint64_t)gr + c > t2.cap) any_ovf = 1;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kRebinEPT; ++u)
+        if (tid + u * kRebinThreads < cnt) sorted[fS[(v[u] >> t2.ts) - fbase] + r[u]] = v[u];
+    __syncthreads();
+    const bool ovf = any_ovf != 0;
+    for (uint32_t j = tid; j < cnt; j += kRebinThreads) {
+        const uint32_t x = sorted[j], f = (x >> t2.ts) - fbase;
+        if (!ovf || j < flim[f]) {
+            b2[fGX[f] + j] = x;
+        } else {  // past the fine bucket's capacity: the spill bitmap
+            __hip_atomic_fetch_or(sc2.spill32 + (x >> 5), 1u << (x & 31), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+            sc2.spill_flag[x >> t2.ts] = 1u;
+        }
     }
 }
 
@@ -853,10 +953,13 @@ int check_common(uint64_t n, uint32_t m, int flavor, const void *keys, const voi
 struct Workspace {
     int dev = -1;
     hipStream_t st = nullptr;
-    uint32_t *zeroed = nullptr;   // gcur [kShards*kMaxTiles] | spill_flag [kMaxTiles] | spill32
+    uint32_t *zeroed = nullptr;   // gcur [kShards*kMaxTiles] | spill_flag [kMaxTiles] |
+                                  // super-tile cursors [kShards*kMaxSuper] | spill32
     size_t zeroed_bytes = 0;
     void *buckets = nullptr;
     size_t bucket_bytes = 0;
+    void *buckets2 = nullptr;     // fine buckets of the two-level build
+    size_t bucket2_bytes = 0;
 };
 std::mutex g_ws_mu;
 std::vector<Workspace *> g_ws;
@@ -879,10 +982,27 @@ constexpr size_t kCurWords = (size_t)kShards * kMaxTiles;
 
 // Grows the workspace (synchronising the stream before freeing old buffers).
 // Not graph-capturable when it has to grow: call once with the largest shape first.
-int ws_reserve(Workspace &w, uint32_t m, size_t bucket_bytes, TileScratch *sc) {
+int grow(Workspace &w, void **buf, size_t *have, size_t want_bytes) {
+    if (want_bytes <= *have) return NB_OK;
+    if (*buf) NB_HIP(hipFree(*buf));
+    *buf = nullptr;
+    *have = 0;
+    const size_t want = want_bytes + want_bytes / 8;
+    NB_HIP(hipMalloc(buf, want));
+    *have = want;
+    return NB_OK;
+}
+
+constexpr size_t kSuperCurWords = (size_t)kShards * kMaxSuper;
+
+// Grows the workspace (synchronising the stream before freeing old buffers).
+// Not graph-capturable when it has to grow: call once with the largest shape first.
+int ws_reserve(Workspace &w, uint32_t m, size_t bucket_bytes, TileScratch *sc,
+               size_t bucket2_bytes = 0) {
     const size_t spill_words32 = 2 * (((size_t)m + 63) / 64);
-    const size_t zb = (kCurWords + kMaxTiles + spill_words32) * 4;
-    if (zb > w.zeroed_bytes || bucket_bytes > w.bucket_bytes) NB_HIP(hipStreamSynchronize(w.st));
+    const size_t zb = (kCurWords + kMaxTiles + kSuperCurWords + spill_words32) * 4;
+    if (zb > w.zeroed_bytes || bucket_bytes > w.bucket_bytes || bucket2_bytes > w.bucket2_bytes)
+        NB_HIP(hipStreamSynchronize(w.st));
     if (zb > w.zeroed_bytes) {
         if (w.zeroed) NB_HIP(hipFree(w.zeroed));
         w.zeroed = nullptr;
@@ -891,19 +1011,18 @@ int ws_reserve(Workspace &w, uint32_t m, size_t bucket_bytes, TileScratch *sc) {
         NB_HIP(hipMemset(w.zeroed, 0, zb));
         w.zeroed_bytes = zb;
     }
-    if (bucket_bytes > w.bucket_bytes) {
-        if (w.buckets) NB_HIP(hipFree(w.buckets));
-        w.buckets = nullptr;
-        w.bucket_bytes = 0;
-        const size_t want = bucket_bytes + bucket_bytes / 8;
-        NB_HIP(hipMalloc(&w.buckets, want));
-        w.bucket_bytes = want;
-    }
+    int rc;
+    if ((rc = grow(w, &w.buckets, &w.bucket_bytes, bucket_bytes)) ||
+        (rc = grow(w, &w.buckets2, &w.bucket2_bytes, bucket2_bytes)))
+        return rc;
     sc->gcur = w.zeroed;
     sc->spill_flag = w.zeroed + kCurWords;
-    sc->spill32 = w.zeroed + kCurWords + kMaxTiles;
+    sc->spill32 = w.zeroed + kCurWords + kMaxTiles + kSuperCurWords;
     return NB_OK;
 }
+
+// the super-tile cursors of the two-level build (zero between builds)
+uint32_t *super_cursors(Workspace &w) { return w.zeroed + kCurWords + kMaxTiles; }
 
 uint32_t env_u32(const char *name, uint32_t dflt) {
     const char *e = std::getenv(name);
@@ -928,6 +1047,20 @@ TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
     cap = (cap + 7) & ~7ull;
     tc.cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFC0ull);
+    tc.fts = ts;
+    return tc;
+}
+
+// Pass 1 of the two-level build: super tiles of kSuperFine fine tiles each.
+TileCfg super_tiles(const TileCfg &fine, uint32_t m, uint64_t n_chunk, uint32_t k) {
+    TileCfg tc = fine;
+    tc.ts = fine.ts + 6;  // log2(kSuperFine)
+    tc.T = (uint32_t)(((uint64_t)m + (1ull << tc.ts) - 1) >> tc.ts);
+    const double e = (double)n_chunk * k / ((double)tc.T * tc.G);
+    uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
+    cap = (cap + 7) & ~7ull;
+    tc.cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFC0ull);
+    tc.fts = fine.ts;
     return tc;
 }
 
@@ -1008,12 +1141,74 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     return NB_OK;
 }
 
+// The two-level build (see bloom_rebin_kernel): per chunk, the bin kernel into
+// super tiles, the re-bin into fine tiles, the tile kernel on the fine tiles.
+template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR>
+int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                     const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st,
+                     uint64_t chunk, const TileCfg &t1, const TileCfg &t2) {
+    constexpr uint64_t kpb = (uint64_t)KPT * NT;
+    Workspace *ws;
+    TileScratch sc;
+    int rc;
+    if ((rc = get_ws(st, &ws))) return rc;
+    if ((rc = ws_reserve(*ws, c.fm.m, (size_t)t1.T * t1.G * t1.cap * 4, &sc,
+                         (size_t)t2.T * t2.G * t2.cap * 4)))
+        return rc;
+    TileScratch sc1 = sc;
+    sc1.gcur = super_cursors(*ws);
+    size_t sort_bytes = kpb * c.k * 4;
+    if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, kStageBytes);
+    const size_t bin_lds = (size_t)bin_sort_offset_words(t1.T) * 4 + sort_bytes;
+    const size_t rebin_lds = (size_t)kRebinSpan * 4;
+    const size_t tile_lds = ((size_t)1 << (t2.ts - 3)) + (2 * kShards + 1) * 4;
+    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, uint32_t, NT, STAGE, KR>;
+    auto tile_ow = bloom_tile_or_kernel<uint32_t, true>;
+    auto tile_or = bloom_tile_or_kernel<uint32_t, false>;
+    if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(tile_ow, tile_lds)) ||
+        (rc = allow_lds(tile_or, tile_lds)))
+        return rc;
+    NB_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(bloom_rebin_kernel),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)rebin_lds));
+    const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
+    uint32_t *b1 = reinterpret_cast<uint32_t *>(ws->buckets);
+    uint32_t *b2 = reinterpret_cast<uint32_t *>(ws->buckets2);
+    const uint32_t rebin_x = (uint32_t)(((uint64_t)t1.cap * t1.G + kRebinSpan - 1) / kRebinSpan);
+    for (uint64_t done = 0; done < n; done += chunk) {
+        const uint64_t cn = std::min(chunk, n - done);
+        const uint8_t *ck = offsets ? keys : keys + done * key_len;
+        const uint64_t *co = offsets ? offsets + done : nullptr;
+        hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st, ck,
+                           co, key_len, cn, c, t1, sc1, b1);
+        NB_HIP(hipGetLastError());
+        hipLaunchKernelGGL(bloom_rebin_kernel, dim3(rebin_x, t1.T), dim3(kRebinThreads), rebin_lds,
+                           st, t1, t2, sc1, sc, b1, b2);
+        NB_HIP(hipGetLastError());
+        NB_HIP(hipMemsetAsync(sc1.gcur, 0, (size_t)t1.G * t1.T * 4, st));  // keep them zero
+        hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(t2.T),
+                           dim3(kTileThreads), tile_lds, st, t2, sc, b2, words, nwords);
+        NB_HIP(hipGetLastError());
+    }
+    return NB_OK;
+}
+
 template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR>
 int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                  const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st) {
     constexpr uint64_t kpb = (uint64_t)KPT * NT;
-    const uint64_t chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, chunk_keys(n, c.k)));
-    const TileCfg tc = choose_tiles(c.fm.m, chunk, c.k);
+    uint64_t chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, chunk_keys(n, c.k)));
+    TileCfg tc = choose_tiles(c.fm.m, chunk, c.k);
+    if (tc.T > 2 * (uint32_t)NT && env_u32("NB_TWO_LEVEL", 1) != 0) {
+        // two bucket arrays of <= ~8 GiB each (u32 entry indices stay in range)
+        const uint64_t budget = std::max<uint64_t>(kpb, (8ull << 30) / (4ull * c.k));
+        const uint64_t passes = (n + budget - 1) / budget;
+        chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, (n + passes - 1) / passes));
+        if (const uint64_t v = env_u32("NB_CHUNK_KEYS", 0)) chunk = std::min<uint64_t>(n, v);
+        tc = choose_tiles(c.fm.m, chunk, c.k);
+        return launch_two_level<FLAVOR, LAYOUT, KPT, NT, STAGE, KR>(
+            keys, offsets, key_len, n, c, words, overwrite, st, chunk,
+            super_tiles(tc, c.fm.m, chunk, c.k), tc);
+    }
     if (tc.ts <= 16 && env_u32("NB_ENTRY32", 0) == 0)
         return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint16_t, NT, STAGE, KR>(
             keys, offsets, key_len, n, c, words, overwrite, st, chunk, tc);
@@ -1196,6 +1391,7 @@ int nb_shutdown(void) {
             (void)hipStreamSynchronize(w->st);
             if (w->zeroed) (void)hipFree(w->zeroed);
             if (w->buckets) (void)hipFree(w->buckets);
+            if (w->buckets2) (void)hipFree(w->buckets2);
             delete w;
         }
         g_ws.clear();

@@ -249,6 +249,41 @@ def test_tiled_bucket_overflow_spill(dev, oracle, monkeypatch):
     np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("two_level", ["1", "0"])
+@pytest.mark.parametrize("chunk", ["0", "300000"])
+def test_two_level_build_large_m(dev, oracle, two_level, chunk, monkeypatch):
+    """m > 2^31 (C5's 2^32-1): 4 096 fine tiles, built through super tiles + re-bin
+    (NB_TWO_LEVEL=1, the default) or binned straight into the fine tiles; chunked
+    builds accumulate across chunks; k = 10 and k = 7 (rank paths KR=16 / KR=8)."""
+    from nasp_bloom import synth
+    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    monkeypatch.setenv("NB_TWO_LEVEL", two_level)
+    if chunk != "0":
+        monkeypatch.setenv("NB_CHUNK_KEYS", chunk)
+    n = 1_000_003
+    buf = synth.fixed_keys(n, 32, seed=77)
+    for m, k in ((2**32 - 1, 10), (3_000_000_019, 7)):
+        got = dev_build(dev, buf, None, 32, n, m, k, SEED)
+        want = oracle.build(0, buf, None, 32, n, m, k, SEED)
+        np.testing.assert_array_equal(got, want)
+    vb, vo = synth.var_keys(300_000)
+    got = dev_build(dev, vb, vo, 0, 300_000, 2**32 - 1, 10, SEED)
+    np.testing.assert_array_equal(got, oracle.build(0, vb, vo, 0, 300_000, 2**32 - 1, 10, SEED))
+
+
+def test_two_level_overflow_spill(dev, oracle, monkeypatch):
+    """Duplicated keys overflow both the super-tile and the fine-tile buckets of the
+    two-level build: pass 1 spills by fine tile, the re-bin spills too."""
+    from nasp_bloom import synth
+    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    n = 400_000
+    buf = np.zeros(n * 32 + 16, np.uint8)
+    buf[: 32 * 5000] = synth.fixed_keys(5000, 32)[: 32 * 5000]
+    got = dev_build(dev, buf, None, 32, n, 2**32 - 1, 10, SEED)
+    want = oracle.build(0, buf, None, 32, n, 2**32 - 1, 10, SEED)
+    np.testing.assert_array_equal(got, want)
+
+
 @pytest.mark.parametrize("chunk", ["4096", "100000", "999999"])
 def test_tiled_chunking(dev, oracle, chunk, monkeypatch):
     from nasp_bloom import synth
