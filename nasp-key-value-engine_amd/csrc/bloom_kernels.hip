@@ -244,6 +244,9 @@ constexpr int kTileThreads = 1024;
 constexpr int kTileUnroll = 4;   // 16-byte bucket loads in flight per lane
 constexpr int kShards = 8;
 constexpr uint32_t kStageBytes = 48 * 1024;  // LDS staging window for variable-length keys
+constexpr uint32_t kLenClasses = 16;         // word-count classes of the staged keys' order
+// the stage is followed by the length permutation: key info [NT] | order [NT] | classes
+constexpr size_t stage_lds_bytes(int nt) { return kStageBytes + (2 * (size_t)nt + kLenClasses) * 4; }
 constexpr uint32_t kMaxTiles = 4096;
 
 // Diagnostic builds (tools/ubench_tiled.hip) stop a kernel after a phase to price
@@ -554,6 +557,12 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
             const uint64_t wb = koff(pb) & ~15ull;
             const uint64_t span = koff(pe) - wb;
             const bool staged = span <= (uint64_t)kStageBytes;  // block-uniform
+            // staged variable-length keys are hashed in order of their word count: a
+            // wave's lanes then loop over like lengths instead of its longest key
+            constexpr bool kPermute = LAYOUT == kOffsets;
+            uint32_t *kinfo = reinterpret_cast<uint32_t *>(stage + kStageBytes);  // [NT]
+            uint32_t *perm = kinfo + NT;                                         // [NT]
+            uint32_t *lhist = perm + NT;                                         // [kLenClasses]
             if (p) __syncthreads();  // the previous sub-batch is hashed: the stage is free
             if (staged) {
                 const uint4 *src = reinterpret_cast<const uint4 *>(keys + wb);
@@ -561,12 +570,35 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
                 const uint32_t nvec = (uint32_t)((span + 15) / 16);
                 for (uint32_t q = tid; q < nvec; q += NT) dst[q] = src[q];
             }
+            if (kPermute && staged && tid < kLenClasses) lhist[tid] = 0;
             __syncthreads();
-            if (i < n) {
+            uint32_t klo = (uint32_t)(b - wb), klen = (uint32_t)(e - b);
+            bool kvalid = i < n;
+            if (kPermute && staged) {
+                // counting sort of the sub-batch by word count (absent keys last)
+                const uint32_t cls = kvalid ? min((klen + 7) >> 3, kLenClasses - 2) : kLenClasses - 1;
+                kinfo[tid] = klo | (klen << 16);  // both < 2^16 inside the stage
+                const uint32_t r = atomicAdd(&lhist[cls], 1u);
+                __syncthreads();
+                if (tid < 64) {
+                    const uint32_t cnt = tid < kLenClasses ? lhist[tid] : 0u;
+                    const uint32_t st = wave_inclusive_scan(cnt) - cnt;
+                    if (tid < kLenClasses) lhist[tid] = st;
+                }
+                __syncthreads();
+                perm[lhist[cls] + r] = tid;
+                __syncthreads();
+                const uint32_t src = perm[tid];  // a key of this sub-batch; valid ones first
+                const uint32_t info = kinfo[src];
+                klo = info & 0xffffu;
+                klen = info >> 16;
+                kvalid = pb + src < n;  // == (i < n): the valid keys fill the first slots
+            }
+            if (kvalid) {
                 uint64_t h1, h2;
-                const uint32_t len = (uint32_t)(e - b);
+                const uint32_t len = klen;
                 if (staged) {
-                    const uint32_t lo = (uint32_t)(b - wb), a = lo & 7u;
+                    const uint32_t lo = klo, a = lo & 7u;
                     const uint64_t *q = reinterpret_cast<const uint64_t *>(stage + (lo - a));
                     auto load = [q](uint32_t j) { return q[j]; };
                     nb::hash_aligned_words<FLAVOR, decltype(load), LAYOUT == kFixedStride>(
@@ -1116,7 +1148,7 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     if ((rc = ws_reserve(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * sizeof(ENTRY), &sc)))
         return rc;
     size_t sort_bytes = kpb * c.k * 4;
-    if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, kStageBytes);
+    if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(NT));
     const size_t bin_lds = (size_t)bin_sort_offset_words(tc.T) * 4 + sort_bytes;
     const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
     auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, ENTRY, NT, STAGE, KR>;
@@ -1158,7 +1190,7 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
     TileScratch sc1 = sc;
     sc1.gcur = super_cursors(*ws);
     size_t sort_bytes = kpb * c.k * 4;
-    if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, kStageBytes);
+    if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(NT));
     const size_t bin_lds = (size_t)bin_sort_offset_words(t1.T) * 4 + sort_bytes;
     const size_t rebin_lds = (size_t)kRebinSpan * 4;
     const size_t tile_lds = ((size_t)1 << (t2.ts - 3)) + (2 * kShards + 1) * 4;
