@@ -11,14 +11,34 @@
 // tests/test_engine_dropin.py checks every filter file against the oracle and the
 // drop-in run against the reference run.
 //
-// usage: engine <data_dir> <raw|comp> <n_records> <block_size> [tiered]
-//   writes one level-1 SSTable of n records ("user%012d" keys); with `tiered`,
-//   writes three tables and runs LSMManager::triggerCompactionCheck
-//   (size-tiered, LSM/LSMManager.cpp:203-233) so a level-2 table is compacted.
+// usage: engine <data_dir> <raw|comp> <n_records> <block_size> [tiered|leveled]
+//   writes one level-1 SSTable of n records ("user%012d" keys); with `tiered` or
+//   `leveled`, writes three overlapping tables and runs
+//   LSMManager::triggerCompactionCheck: size-tiered (LSM/LSMManager.cpp:203-233,
+//   the level is merged into one level-2 table) or leveled (LSMManager.cpp:146-196,
+//   multiplier 2: two level-1 tables are merged one by one into level 2).
+// NB_ENGINE_TIME (seconds) fixes the clock the filters' timeConst comes from
+// (BloomFilter.cpp:37): runs of both binaries then write byte-identical files.
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <string>
 #include <vector>
+
+// time() for this executable's own code (the BloomFilter constructors compiled
+// into it resolve to this definition before libc's).
+extern "C" time_t time(time_t *out) {
+    const char *fixed = std::getenv("NB_ENGINE_TIME");
+    const time_t v = fixed && *fixed
+                         ? (time_t)std::strtoll(fixed, nullptr, 10)
+                         : (time_t)std::chrono::duration_cast<std::chrono::seconds>(
+                               std::chrono::system_clock::now().time_since_epoch())
+                               .count();
+    if (out) *out = v;
+    return v;
+}
 
 #include "Config.h"
 #include "LSMManager.h"
@@ -46,7 +66,7 @@ static std::vector<Record> records(int first, int n) {
 
 int main(int argc, char **argv) {
     if (argc < 5) {
-        std::fprintf(stderr, "usage: %s <dir> <raw|comp> <n> <block_size> [tiered]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s <dir> <raw|comp> <n> <block_size> [tiered|leveled]\n", argv[0]);
         return 2;
     }
     Config::data_directory = argv[1];
@@ -55,13 +75,16 @@ int main(int argc, char **argv) {
     const int n = std::atoi(argv[3]);
     Config::block_size = std::atoi(argv[4]);
     const bool tiered = argc > 5 && std::strcmp(argv[5], "tiered") == 0;
-    Config::compaction_strategy = "tiered";
+    const bool leveled = argc > 5 && std::strcmp(argv[5], "leveled") == 0;
+    Config::compaction_strategy = leveled ? "leveled" : "tiered";
     Config::max_levels = 4;
     Config::max_number_of_sstable_on_level = 3;
+    Config::l0_compaction_trigger = 2;
+    Config::level_size_multiplier = 2;
 
     Block_manager bm;
     SSTManager sst(&bm);
-    if (!tiered) {
+    if (!tiered && !leveled) {
         sst.write(records(0, n), 1);
     } else {
         for (int t = 0; t < 3; ++t) sst.write(records(t * (n / 2), n), 1);  // overlapping ranges

@@ -34,9 +34,13 @@ def keys_for(n_tables, n):
     return [b"user%012d" % i for i in idx]
 
 
-def run_engine(exe, d, mode, n, bs, tiered=False):
-    args = [exe, str(d), mode, str(n), str(bs)] + (["tiered"] if tiered else [])
-    out = subprocess.run(args, capture_output=True, timeout=600)  # the engine prints raw bytes
+def run_engine(exe, d, mode, n, bs, tiered=False, compaction=None, fixed_time=None):
+    comp = compaction or ("tiered" if tiered else None)
+    args = [exe, str(d), mode, str(n), str(bs)] + ([comp] if comp else [])
+    env = dict(os.environ)
+    if fixed_time is not None:
+        env["NB_ENGINE_TIME"] = str(fixed_time)  # the filters' timeConst (harness clock)
+    out = subprocess.run(args, capture_output=True, timeout=600, env=env)  # prints raw bytes
     if out.returncode != 0:
         err = out.stderr[-2000:].decode(errors="replace")
         raise AssertionError(f"{exe} failed rc={out.returncode}: {err}")
@@ -158,3 +162,29 @@ def test_engine_with_dropin_on_gpu(tmp_path, oracle, mode, tiered, built):
         assert metas, others(d_ref)
         for f in others(d_ref):
             assert open(d_ref / f, "rb").read() == open(d_new / f, "rb").read(), f
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["raw", "comp"])
+@pytest.mark.parametrize("compaction", [None, "tiered", "leveled"])
+def test_engine_every_file_identical_on_gpu(tmp_path, mode, compaction, built):
+    """With the harness clock fixed (so both runs draw the same timeConst and h2_seed,
+    BloomFilter.cpp:37-46), the reference engine on the drop-in BloomFilter and
+    MerkleTree writes exactly the files the reference engine writes -- filters
+    included, byte for byte -- through flush, size-tiered and leveled compaction
+    (LSMManager.cpp:146-233)."""
+    if not (os.path.exists(DROPIN_ENGINE) and os.path.exists(REF_ENGINE)):
+        pytest.skip("engine binaries not built (need /root/reference at build time)")
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n, bs, t = 3000, 4096, 1748963255
+    d_ref, d_new = tmp_path / "ref", tmp_path / "dropin"
+    run_engine(REF_ENGINE, d_ref, mode, n, bs, compaction=compaction, fixed_time=t)
+    run_engine(DROPIN_ENGINE, d_new, mode, n, bs, compaction=compaction, fixed_time=t)
+    files = lambda d: sorted(os.path.relpath(os.path.join(r, f), d) for r, _, fs in os.walk(d)
+                             for f in fs)
+    assert files(d_ref) == files(d_new)
+    assert len(filter_files(d_ref)) == {None: 1, "tiered": 1, "leveled": 3}[compaction]
+    for f in files(d_ref):
+        assert open(d_ref / f, "rb").read() == open(d_new / f, "rb").read(), f
