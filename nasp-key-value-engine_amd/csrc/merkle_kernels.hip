@@ -5,7 +5,7 @@
 //
 //   leaves : one lane per record, H(record) with the filter's word-stream hash
 //            (bloom_math.h hash1_aligned_words), into tree[0..n)
-//   levels : one 1024-thread block per 2048 nodes, up to 11 levels per launch in
+//   levels : one 256-thread block per 512 nodes, up to 3 levels per launch in
 //            LDS: parent i = H(to_string(node 2i) ++ to_string(node 2i+1)), the
 //            last node of an odd level paired with itself (merkle.cpp:44-48);
 //            every level is stored into the tree (generateProof's treeLevels)
@@ -23,10 +23,19 @@ int nb_internal_fail(int code, const char *msg);  // bloom_kernels.hip
 
 namespace {
 
+// Level-kernel geometry (tools/ubench_merkle.hip, C2's 10M records): a block
+// halves its busy threads every level, so long in-LDS chains idle most lanes --
+// 1 024 threads x 11 levels took 0.356 ms, 256 threads x 3 levels 0.224 ms.
+#ifndef NB_MERKLE_THREADS
+#define NB_MERKLE_THREADS 256
+#endif
+#ifndef NB_MERKLE_SUBLEVELS
+#define NB_MERKLE_SUBLEVELS 3
+#endif
 constexpr int kLeafBlock = 256;
-constexpr int kLevelThreads = 1024;
+constexpr int kLevelThreads = NB_MERKLE_THREADS;
 constexpr int kLevelSpan = 2 * kLevelThreads;  // nodes read per block
-constexpr int kMaxSub = 11;                    // log2(kLevelSpan) levels per launch
+constexpr int kMaxSub = NB_MERKLE_SUBLEVELS;   // levels per launch (<= log2(kLevelSpan))
 
 template <int FLAVOR, bool OFFSETS>
 __global__ __launch_bounds__(kLeafBlock) void merkle_leaf_kernel(
