@@ -44,6 +44,8 @@ def run_engine(exe, d, mode, n, bs, tiered=False, compaction=None, fixed_time=No
     if out.returncode != 0:
         err = out.stderr[-2000:].decode(errors="replace")
         raise AssertionError(f"{exe} failed rc={out.returncode}: {err}")
+    m = re.search(rb"engine_ms ([0-9.]+)", out.stderr)
+    return float(m.group(1)) if m else None
 
 
 def filter_files(d):
@@ -188,3 +190,26 @@ def test_engine_every_file_identical_on_gpu(tmp_path, mode, compaction, built):
     assert len(filter_files(d_ref)) == {None: 1, "tiered": 1, "leveled": 3}[compaction]
     for f in files(d_ref):
         assert open(d_ref / f, "rb").read() == open(d_new / f, "rb").read(), f
+
+
+@pytest.mark.gpu
+def test_engine_large_flush_identical_on_gpu(tmp_path, built):
+    """One 300 000-record flush (SSTManager::write, raw) through both engines: every
+    file byte-identical; prints both engine times (harness clock around
+    SSTManager::write only) -- the drop-ins remove the filter and Merkle share of a
+    flush, the rest is the engine's own block I/O."""
+    if not (os.path.exists(DROPIN_ENGINE) and os.path.exists(REF_ENGINE)):
+        pytest.skip("engine binaries not built (need /root/reference at build time)")
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n, bs, t = 300_000, 4096, 1748963255
+    d_ref, d_new = tmp_path / "ref", tmp_path / "dropin"
+    ms_ref = run_engine(REF_ENGINE, d_ref, "raw", n, bs, fixed_time=t)
+    ms_new = run_engine(DROPIN_ENGINE, d_new, "raw", n, bs, fixed_time=t)
+    files = lambda d: sorted(os.path.relpath(os.path.join(r, f), d) for r, _, fs in os.walk(d)
+                             for f in fs)
+    assert files(d_ref) == files(d_new)
+    for f in files(d_ref):
+        assert open(d_ref / f, "rb").read() == open(d_new / f, "rb").read(), f
+    print(f"\nengine flush of {n} records: reference {ms_ref:.1f} ms, drop-in {ms_new:.1f} ms")
