@@ -83,6 +83,17 @@ int nb_build(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uin
              uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
              uint64_t *words, int device);
 
+/* Single-process multi-GPU nb_build (the C++ host's form of the cooperative C5
+ * build, §8(e)): keys split into `nshards` contiguous ranges (<= 0: one per visible
+ * device), shard s built on device s % device_count by its own streaming builder
+ * and host thread; the partial filters are OR-merged slice-wise -- owner o pulls
+ * word slice o of every other partial over xGMI (peer copies), ORs them in
+ * (nb_or_merge_device) and downloads its slice into `words`.  Same result and
+ * OR-accumulate semantics as nb_build. */
+int nb_build_sharded(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                     uint32_t m, uint32_t k, uint64_t h2_seed, int flavor, uint64_t *words,
+                     int nshards);
+
 /* Batch form of BloomFilter::possiblyContains (BloomFilter.cpp:67-80):
  * out[i] = 1 if all k bits of key i are set, else 0.  k == 0 answers 1
  * (the default-constructed filter, BloomFilter.cpp:26). */

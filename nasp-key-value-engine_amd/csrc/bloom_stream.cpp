@@ -17,6 +17,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/nasp_bloom.h"
@@ -330,6 +331,121 @@ int nb_builder_destroy(nb_builder *b) {
 }
 
 }  // extern "C"
+
+namespace {
+
+// Everything added so far is built: the partial chunk submitted, the stream drained.
+int drain(nb_builder *b) {
+    SB_HIP(hipSetDevice(b->ss->dev));
+    const int rc = b->submit();
+    if (rc) return rc;
+    SB_HIP(hipStreamSynchronize(b->ss->comp));
+    for (Slot &sl : b->ss->s) sl.busy = false;
+    return NB_OK;
+}
+
+// Owner o's step of the merge: OR slice [lo, lo + len) of every other partial into
+// its own (peer copies over xGMI into one staging buffer, one OR launch), then
+// download the merged slice into the caller's words.
+int merge_slice(std::vector<nb_builder *> &bs, int o, uint64_t lo, uint64_t len, uint64_t *words) {
+    nb_builder *own = bs[o];
+    const int dev = own->ss->dev;
+    hipStream_t st = own->ss->comp;
+    SB_HIP(hipSetDevice(dev));
+    const uint32_t nsrc = (uint32_t)bs.size() - 1;
+    uint64_t *tmp = nullptr;
+    if (nsrc) {
+        SB_HIP(hipMalloc(&tmp, nsrc * len * 8));
+        uint32_t j = 0;
+        for (size_t s = 0; s < bs.size(); ++s) {
+            if ((int)s == o) continue;
+            const hipError_t e = hipMemcpyPeerAsync(tmp + (j++) * len, dev, bs[s]->ss->d_words + lo,
+                                                    bs[s]->ss->dev, len * 8, st);
+            if (e != hipSuccess) {
+                (void)hipFree(tmp);
+                return nb_internal_fail(NB_ERR_HIP, (std::string("hipMemcpyPeerAsync: ") +
+                                                     hipGetErrorString(e)).c_str());
+            }
+        }
+        const int rc = nb_or_merge_device(own->ss->d_words + lo, tmp, len, nsrc, len, st);
+        if (rc) {
+            (void)hipStreamSynchronize(st);
+            (void)hipFree(tmp);
+            return rc;
+        }
+    }
+    const hipError_t e1 = hipMemcpyAsync(words + lo, own->ss->d_words + lo, len * 8,
+                                         hipMemcpyDeviceToHost, st);
+    const hipError_t e2 = hipStreamSynchronize(st);
+    if (tmp) (void)hipFree(tmp);
+    SB_HIP(e1);
+    SB_HIP(e2);
+    return NB_OK;
+}
+
+}  // namespace
+
+extern "C" int nb_build_sharded(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
+                                uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
+                                uint64_t *words, int nshards) {
+    if (flavor != NB_FLAVOR_LIBSTDCXX && flavor != NB_FLAVOR_MSVC_FNV1A)
+        return nb_internal_fail(NB_ERR_ARG, "unknown flavor");
+    if (n && m == 0) return nb_internal_fail(NB_ERR_ARG, "m == 0 with keys (reference divides by zero)");
+    if (n && (!keys || !words)) return nb_internal_fail(NB_ERR_ARG, "NULL keys or words");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        return nb_internal_fail(NB_ERR_NODEV, "no HIP device visible");
+    if (nshards <= 0) nshards = count;
+    if (n == 0 || k == 0) return NB_OK;
+    if (nshards == 1) return nb_build(keys, offsets, key_len, n, m, k, h2_seed, flavor, words, 0);
+    // direct xGMI peer copies where the devices allow them (already-enabled pairs
+    // report an error that is not one; clear it so no later check sees it)
+    const int ndev = std::min(nshards, count);
+    for (int a = 0; a < ndev; ++a) {
+        (void)hipSetDevice(a);
+        for (int b = 0; b < ndev; ++b) {
+            int can = 0;
+            if (a != b && hipDeviceCanAccessPeer(&can, a, b) == hipSuccess && can)
+                (void)hipDeviceEnablePeerAccess(b, 0);
+        }
+        (void)hipGetLastError();
+    }
+    // phase 1: shard s = keys [n s / S, n (s+1) / S) on device s % count, one host
+    // thread each; shard 0's filter starts from the caller's bits
+    std::vector<nb_builder *> bs(nshards, nullptr);
+    std::vector<int> rcs(nshards, NB_OK);
+    std::vector<std::string> msgs(nshards);
+    auto run_shard = [&](int s) {
+        const uint64_t b = n * (uint64_t)s / nshards, e = n * (uint64_t)(s + 1) / nshards;
+        int rc = nb_builder_create(m, k, h2_seed, flavor, s == 0 ? words : nullptr, s % count, &bs[s]);
+        if (!rc && e > b)
+            rc = offsets ? nb_builder_add_batch(bs[s], keys, offsets + b, 0, e - b)
+                         : nb_builder_add_batch(bs[s], keys + b * key_len, nullptr, key_len, e - b);
+        if (!rc) rc = drain(bs[s]);
+        if (rc) msgs[s] = nb_last_error();
+        rcs[s] = rc;
+    };
+    auto run_all = [&](auto &&fn) {
+        std::vector<std::thread> th;
+        for (int s = 0; s < nshards; ++s) th.emplace_back(fn, s);
+        for (auto &t : th) t.join();
+        for (int s = 0; s < nshards; ++s)
+            if (rcs[s]) return nb_internal_fail(rcs[s], msgs[s].c_str());
+        return (int)NB_OK;
+    };
+    int rc = run_all(run_shard);
+    // phase 2: owner o merges and downloads word slice o
+    if (!rc) {
+        const uint64_t nw = ((uint64_t)m + 63) / 64;
+        rc = run_all([&](int o) {
+            const uint64_t lo = nw * (uint64_t)o / nshards, hi = nw * (uint64_t)(o + 1) / nshards;
+            rcs[o] = hi > lo ? merge_slice(bs, o, lo, hi - lo, words) : NB_OK;
+            if (rcs[o]) msgs[o] = nb_last_error();
+        });
+    }
+    for (nb_builder *b : bs) (void)nb_builder_destroy(b);
+    return rc;
+}
 
 // Release the pooled slot sets (called by nb_shutdown).
 void nb_internal_stream_shutdown() {

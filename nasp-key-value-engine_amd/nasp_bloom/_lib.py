@@ -35,6 +35,8 @@ _SIGS = {
     "nb_std_hash": (C.c_uint64, [C.c_void_p, C.c_uint64, C.c_int]),
     "nb_build": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
                            C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_int]),
+    "nb_build_sharded": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
+                                   C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_int]),
     "nb_probe": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
                            C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p, C.c_int]),
     "nb_build_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,

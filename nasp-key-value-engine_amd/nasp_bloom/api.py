@@ -100,6 +100,16 @@ def build_host(keys: np.ndarray, offsets: np.ndarray | None, key_len: int, n: in
     check(rc, "nb_build")
 
 
+def build_host_sharded(keys: np.ndarray, offsets: np.ndarray | None, key_len: int, n: int, m: int,
+                       k: int, seed: int, flavor: int, words: np.ndarray, nshards: int = 0) -> None:
+    """nb_build over `nshards` key ranges (0: one per visible device), shard s on
+    device s % device_count, partials OR-merged over xGMI into the host words."""
+    assert words.dtype == np.uint64 and words.flags.c_contiguous
+    rc = lib().nb_build_sharded(_np_ptr(keys), _np_ptr(offsets), key_len, n, m, k, seed, flavor,
+                                _np_ptr(words), nshards)
+    check(rc, "nb_build_sharded")
+
+
 def probe_host(keys: np.ndarray, offsets: np.ndarray | None, key_len: int, n: int, m: int, k: int,
                seed: int, flavor: int, words: np.ndarray, device: int = 0) -> np.ndarray:
     out = np.zeros(max(n, 1), dtype=np.uint8)
