@@ -18,6 +18,7 @@ bounded sample of the same workload, 1 core).
 from __future__ import annotations
 
 import argparse
+import contextlib
 import glob
 import json
 import os
@@ -35,6 +36,19 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level para
 def algorithmic_bytes(n, key_len, total_key_bytes, m, var_len):
     """keys read once, offsets read once, the filter written once."""
     return total_key_bytes + (8 * (n + 1) if var_len else 0) + (m + 7) // 8
+
+
+@contextlib.contextmanager
+def pinned_one_core():
+    """Run the calling thread on one core (the 1-core CPU reference,
+    taskset-style); the previous affinity is restored afterwards."""
+    allowed = os.sched_getaffinity(0)
+    core = min(allowed)
+    os.sched_setaffinity(0, {core})
+    try:
+        yield core
+    finally:
+        os.sched_setaffinity(0, allowed)
 
 
 def cpu_baseline(wl, keys_np, offs_np, key_len, budget_s=12.0):
@@ -61,16 +75,17 @@ def cpu_baseline(wl, keys_np, offs_np, key_len, budget_s=12.0):
         Oracle().build(0, keys_np, offs_np, key_len, nk, wl.m, wl.k, H2_SEED)
         return time.perf_counter() - t0
 
-    t_cal = run(n_cal)
-    n_s = int(min(wl.n, max(n_cal, n_cal * budget_s / max(t_cal, 1e-9))))
-    t = run(n_s)
+    with pinned_one_core() as core:
+        t_cal = run(n_cal)
+        n_s = int(min(wl.n, max(n_cal, n_cal * budget_s / max(t_cal, 1e-9))))
+        t = run(n_s)
     try:
         cpu_model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
     except Exception:  # noqa: BLE001
         cpu_model = "unknown"
     return {"value": round(n_s / t / 1e6, 4), "unit": "Mkeys/s", "cores": 1, "kind": kind,
             "sample": f"first {n_s} keys of {wl.name} into the same m={wl.m}, k={wl.k} filter; "
-                      f"reference add() loop, {t:.1f} s, 1 thread ({cpu_model})"}
+                      f"reference add() loop, {t:.1f} s, 1 thread pinned to cpu {core} ({cpu_model})"}
 
 
 def host_path_rate(wl, keys_np, offs_np, key_len, seed, flavor, reps=3):
@@ -363,13 +378,14 @@ def bench_merkle(args, world, rank, dev):
             from oracle_ctypes import RefMerkle
             ref = RefMerkle()
             n_cal = 200_000
-            t_cal, _ = ref.merkle_timed(keys_np, None, kl, n_cal)
-            n_s = int(min(wl.n, max(n_cal, n_cal * args.cpu_budget / max(t_cal, 1e-9))))
-            t_s, _ = ref.merkle_timed(keys_np, None, kl, n_s)
+            with pinned_one_core() as core:
+                t_cal, _ = ref.merkle_timed(keys_np, None, kl, n_cal)
+                n_s = int(min(wl.n, max(n_cal, n_cal * args.cpu_budget / max(t_cal, 1e-9))))
+                t_s, _ = ref.merkle_timed(keys_np, None, kl, n_s)
             out["cpu_baseline"] = {"value": round(n_s / t_s / 1e6, 4), "unit": "Mrecords/s",
                                    "cores": 1, "kind": "reference",
                                    "sample": f"first {n_s} records: reference MerkleTree(data) "
-                                             f"constructor, {t_s:.1f} s, 1 thread"}
+                                             f"constructor, {t_s:.1f} s, 1 thread pinned to cpu {core}"}
         except FileNotFoundError:
             pass
     if rank == 0:
