@@ -133,7 +133,9 @@ int nb_builder_destroy(nb_builder *b);
  * No host synchronisation once the library's per-(device, stream) workspace is
  * large enough; the first call with a larger shape grows it (hipMalloc, stream
  * synchronised), so warm a stream up with its largest shape before capturing it
- * into a hipGraph. */
+ * into a hipGraph.  Key memory is read only in aligned 8- and 16-byte granules
+ * that hold key bytes, so a key buffer needs no slack past its last byte and
+ * may start at any alignment (16-byte-aligned 16-byte keys take a faster path). */
 int nb_build_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
                     uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
                     uint64_t *d_words, void *stream);

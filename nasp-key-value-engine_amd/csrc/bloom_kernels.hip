@@ -554,8 +554,13 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
                 b = koff(i);
                 e = koff(i + 1);
             }
-            const uint64_t wb = koff(pb) & ~15ull;
-            const uint64_t span = koff(pe) - wb;
+            // the stage copy starts at the 16-byte-aligned address at or below the
+            // sub-batch's first key byte: every vector it loads then holds a byte of
+            // the caller's key range (or shares its 16-byte granule), so no load
+            // crosses into an unmapped page, however the key buffer is aligned
+            const uint64_t kb0 = koff(pb);
+            const uint32_t a0 = (uint32_t)((reinterpret_cast<uintptr_t>(keys) + kb0) & 15u);
+            const uint64_t span = koff(pe) - kb0 + a0;
             const bool staged = span <= (uint64_t)kStageBytes;  // block-uniform
             // staged variable-length keys are hashed in order of their word count: a
             // wave's lanes then loop over like lengths instead of its longest key
@@ -565,14 +570,14 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
             uint32_t *lhist = perm + NT;                                         // [kLenClasses]
             if (p) __syncthreads();  // the previous sub-batch is hashed: the stage is free
             if (staged) {
-                const uint4 *src = reinterpret_cast<const uint4 *>(keys + wb);
+                const uint4 *src = reinterpret_cast<const uint4 *>(keys + kb0 - a0);
                 uint4 *dst = reinterpret_cast<uint4 *>(stage);
                 const uint32_t nvec = (uint32_t)((span + 15) / 16);
                 for (uint32_t q = tid; q < nvec; q += NT) dst[q] = src[q];
             }
             if (kPermute && staged && tid < kLenClasses) lhist[tid] = 0;
             __syncthreads();
-            uint32_t klo = (uint32_t)(b - wb), klen = (uint32_t)(e - b);
+            uint32_t klo = (uint32_t)(b - kb0 + a0), klen = (uint32_t)(e - b);
             bool kvalid = i < n;
             if (kPermute && staged) {
                 // counting sort of the sub-batch by word count (absent keys last)
