@@ -48,20 +48,30 @@ def _stream_handle(stream) -> int | None:
     return getattr(stream, "cuda_stream", stream)
 
 
-def _check_device_args(keys, offsets, words):
+def _check_device_args(keys, offsets, words, key_len=0, n=0):
+    """Host-side shape checks before a kernel reads the tensors (no device sync:
+    the last offset itself is the caller's contract)."""
     if not keys.is_cuda or not words.is_cuda:
         raise NaspBloomError("device entry points need CUDA (HIP) tensors")
     if offsets is not None and not offsets.is_cuda:
         raise NaspBloomError("offsets must be on the device")
     if not words.is_contiguous() or not keys.is_contiguous():
         raise NaspBloomError("keys and words must be contiguous")
+    if offsets is None:
+        if keys.numel() * keys.element_size() < n * key_len:
+            raise NaspBloomError(f"keys tensor holds fewer than n * key_len = {n * key_len} bytes")
+    elif n:
+        if offsets.element_size() != 8 or not offsets.is_contiguous():
+            raise NaspBloomError("offsets must be a contiguous 64-bit tensor")
+        if offsets.numel() < n + 1:
+            raise NaspBloomError(f"offsets tensor needs n + 1 = {n + 1} entries")
 
 
 def build_device(keys, offsets, key_len: int, n: int, m: int, k: int, seed: int, flavor: int,
                  words, stream=None, overwrite: bool = False) -> None:
     """OR the k bits of n device-resident keys into `words` (int64/uint64 cuda tensor);
     with overwrite=True, `words` becomes the filter of this batch alone."""
-    _check_device_args(keys, offsets, words)
+    _check_device_args(keys, offsets, words, key_len, n)
     if words.numel() * words.element_size() < nwords(m) * 8:
         raise NaspBloomError("words tensor smaller than ceil(m/64) u64 words")
     rc = lib().nb_build_device_ex(keys.data_ptr(),
@@ -74,7 +84,11 @@ def build_device(keys, offsets, key_len: int, n: int, m: int, k: int, seed: int,
 def probe_device(keys, offsets, key_len: int, n: int, m: int, k: int, seed: int, flavor: int,
                  words, out, stream=None) -> None:
     """out[i] (uint8 cuda tensor) = 1 if all k bits of key i are set."""
-    _check_device_args(keys, offsets, words)
+    _check_device_args(keys, offsets, words, key_len, n)
+    if k and words.numel() * words.element_size() < nwords(m) * 8:
+        raise NaspBloomError("words tensor smaller than ceil(m/64) u64 words")
+    if not out.is_cuda or out.numel() * out.element_size() < n:
+        raise NaspBloomError("out must be a device tensor of at least n bytes")
     rc = lib().nb_probe_device(keys.data_ptr(), offsets.data_ptr() if offsets is not None else None,
                                key_len, n, m, k, seed, flavor, words.data_ptr(), out.data_ptr(),
                                _stream_handle(stream))

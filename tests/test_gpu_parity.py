@@ -233,6 +233,33 @@ def test_empty_and_degenerate(dev, oracle, build_path):
     assert dev_probe(dev, np.zeros(48, np.uint8), None, 16, 3, 1000, 0, SEED, w0).tolist() == [1, 1, 1]
 
 
+def test_device_shape_checks(dev):
+    """Tensors too small for (n, key_len, m) are refused on the host, before any
+    kernel could read past them."""
+    import nasp_bloom as nbm
+    import torch
+    kt = torch.zeros(16 * 10, dtype=torch.uint8, device=dev)
+    wt = torch.zeros(nbm.nwords(1000), dtype=torch.int64, device=dev)
+    out = torch.zeros(11, dtype=torch.uint8, device=dev)
+    offs = torch.zeros(11, dtype=torch.int64, device=dev)
+    for call in (lambda: nbm.build_device(kt, None, 16, 11, 1000, 7, SEED, 0, wt),
+                 lambda: nbm.build_device(kt, offs[:10], 0, 10 + 1, 1000, 7, SEED, 0, wt),
+                 lambda: nbm.build_device(kt, offs.to(torch.int32), 0, 10, 1000, 7, SEED, 0, wt),
+                 lambda: nbm.build_device(kt, None, 16, 10, 100_000, 7, SEED, 0, wt),
+                 lambda: nbm.probe_device(kt, None, 16, 11, 1000, 7, SEED, 0, wt, out),
+                 lambda: nbm.probe_device(kt, None, 16, 10, 1000, 7, SEED, 0, wt, out[:9]),
+                 lambda: nbm.probe_device(kt, None, 16, 10, 100_000, 7, SEED, 0, wt, out)):
+        with pytest.raises(nbm.NaspBloomError):
+            call()
+    nbm.build_device(kt, None, 16, 10, 1000, 7, SEED, 0, wt)  # exact sizes are fine
+    nbm.build_device(kt, offs, 0, 10, 1000, 7, SEED, 0, wt)
+    for o, kl in ((None, 16), (offs, 0)):
+        out.zero_()
+        nbm.probe_device(kt, o, kl, 10, 1000, 7, SEED, 0, wt, out)
+        torch.cuda.synchronize()
+        assert int(out[:10].min()) == 1
+
+
 @pytest.mark.parametrize("k", [1, 8, 9, 16, 17, 24, 32, 33])
 def test_k_range_tiled(dev, oracle, k, monkeypatch):
     """k selects the tiled kernel's keys per block (<=8, <=16, <=32) or the atomic path (>32)."""
