@@ -1,4 +1,4 @@
-"""Multi-process (world size 2, gloo, CPU) tests of the multi-GPU host logic in
+"""Multi-process (world sizes 2-4, gloo, CPU) tests of the multi-GPU host logic in
 nasp_bloom/distributed.py: key sharding, the all-to-all + OR reduce-scatter that
 replaces the missing RCCL bitwise-OR, and the all-gather.  The per-rank build
 step is the oracle here (test-side builder: no GPU in this container); on the
@@ -81,11 +81,14 @@ def _partial(kb, ob, key_len, n, m, k, world):
     return p
 
 
-@pytest.mark.parametrize("var,m,k", [(True, 1_000_003, 7), (False, 95_851, 10), (True, 64, 3)])
-def test_cooperative_or_merge_gloo(tmp_path, oracle, var, m, k):
+@pytest.mark.parametrize("var,m,k,world", [(True, 1_000_003, 7, 2), (False, 95_851, 10, 2),
+                                           (True, 64, 3, 2), (False, 95_851, 7, 3),
+                                           (True, 200_003, 7, 4)])
+def test_cooperative_or_merge_gloo(tmp_path, oracle, var, m, k, world):
+    """World sizes 2-4 (uneven key shards, word slices that do not divide m)."""
     from nasp_bloom import distributed as D
     from nasp_bloom import synth
-    n, world = 30_011, 2
+    n = 30_011
     mp.spawn(_worker, args=(world, _free_port(), n, m, k, var, str(tmp_path)), nprocs=world)
     if var:
         buf, offs = synth.var_keys(n, 0, 40)
