@@ -187,8 +187,14 @@ class RefLib:
                            _ptr(init), _ptr(out))
         return out.tobytes()
 
-    def build_timed(self, keys_u8, offsets, key_len, n, m, k, seed) -> tuple[float, bytes]:
-        """Seconds spent in the reference add() loop, and the serialized image."""
+    def build_timed(self, keys_u8, offsets, key_len, n, m, k, seed,
+                    want_image: bool = True) -> tuple[float, bytes | None]:
+        """Seconds spent in the reference add() loop, and the serialized image
+        (skipped with want_image=False).  Releases the GIL while it runs."""
+        if not want_image:
+            secs = self.lib.ref_build_timed(_ptr(keys_u8), _ptr(offsets, _u64p), key_len, n, m, k,
+                                            seed, None, 0)
+            return secs, None
         size = 28 + ((m + 7) & 0xFFFFFFFF) // 8
         out = np.zeros(size, dtype=np.uint8)
         secs = self.lib.ref_build_timed(_ptr(keys_u8), _ptr(offsets, _u64p), key_len, n, m, k,
