@@ -954,6 +954,23 @@ __global__ __launch_bounds__(kBlock) void or_merge_kernel(uint64_t *__restrict__
     }
 }
 
+// dst[w] |= src_0[w] | ... | src_{n-1}[w], the sources read in place: other
+// allocations on this device, or peer devices' memory over xGMI once peer access
+// is enabled (nb_build_sharded's slice merge).  Up to kGatherSrcs per launch.
+constexpr int kGatherSrcs = 16;
+struct GatherSrcs {
+    const uint64_t *p[kGatherSrcs];
+};
+__global__ __launch_bounds__(kBlock) void or_gather_kernel(uint64_t *__restrict__ dst, GatherSrcs s,
+                                                           uint32_t nsrc, uint64_t nwords) {
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t w = (uint64_t)blockIdx.x * kBlock + threadIdx.x; w < nwords; w += stride) {
+        uint64_t v = dst[w];
+        for (uint32_t i = 0; i < nsrc; ++i) v |= s.p[i][w];
+        dst[w] = v;
+    }
+}
+
 // ------------------------------------------------------------ host side ----
 
 thread_local std::string g_last_error;
@@ -1404,6 +1421,20 @@ int nb_internal_build(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t
     return launch_build(d_keys, d_offsets, key_len, n, m, k, seed, flavor, d_words, overwrite, st);
 }
 int nb_internal_fail(int code, const char *msg) { return fail(code, msg); }
+
+// Launches or_gather_kernel over the sources in groups (stream-ordered).
+int nb_internal_or_gather(uint64_t *dst, const uint64_t *const *srcs, uint32_t nsrc, uint64_t nwords,
+                          hipStream_t st) {
+    for (uint32_t b = 0; b < nsrc && nwords; b += kGatherSrcs) {
+        GatherSrcs g{};
+        const uint32_t cnt = std::min<uint32_t>(kGatherSrcs, nsrc - b);
+        for (uint32_t i = 0; i < cnt; ++i) g.p[i] = srcs[b + i];
+        hipLaunchKernelGGL(or_gather_kernel, dim3(grid_for(nwords)), dim3(kBlock), 0, st, dst, g,
+                           cnt, nwords);
+        NB_HIP(hipGetLastError());
+    }
+    return NB_OK;
+}
 void nb_internal_stream_shutdown();  // bloom_stream.cpp: releases the builders' slot pool
 
 // =================================================================== C ABI ==

@@ -26,6 +26,8 @@ int nb_internal_build(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t
                       uint64_t n, uint32_t m, uint32_t k, uint64_t seed, int flavor,
                       uint64_t *d_words, bool overwrite, hipStream_t st);  // bloom_kernels.hip
 int nb_internal_fail(int code, const char *msg);
+int nb_internal_or_gather(uint64_t *dst, const uint64_t *const *srcs, uint32_t nsrc, uint64_t nwords,
+                          hipStream_t st);  // bloom_kernels.hip
 
 namespace {
 
@@ -344,40 +346,45 @@ int drain(nb_builder *b) {
     return NB_OK;
 }
 
-// Owner o's step of the merge: OR slice [lo, lo + len) of every other partial into
-// its own (peer copies over xGMI into one staging buffer, one OR launch), then
-// download the merged slice into the caller's words.
-int merge_slice(std::vector<nb_builder *> &bs, int o, uint64_t lo, uint64_t len, uint64_t *words) {
+// Owner o's step of the merge: OR word slice [lo, lo + len) of every other
+// partial into its own, reading the sources in place (same device, or a peer over
+// xGMI with peer access enabled) in one stream-ordered kernel, then download the
+// merged slice into the caller's words.  A source the owner cannot address
+// directly is first brought over with a blocking hipMemcpyPeer.
+int merge_slice(std::vector<nb_builder *> &bs, int o, uint64_t lo, uint64_t len, uint64_t *words,
+                const std::vector<char> &peer, int ndev) {
     nb_builder *own = bs[o];
     const int dev = own->ss->dev;
     hipStream_t st = own->ss->comp;
     SB_HIP(hipSetDevice(dev));
-    const uint32_t nsrc = (uint32_t)bs.size() - 1;
+    std::vector<const uint64_t *> srcs;
     uint64_t *tmp = nullptr;
-    if (nsrc) {
-        SB_HIP(hipMalloc(&tmp, nsrc * len * 8));
-        uint32_t j = 0;
-        for (size_t s = 0; s < bs.size(); ++s) {
-            if ((int)s == o) continue;
-            const hipError_t e = hipMemcpyPeerAsync(tmp + (j++) * len, dev, bs[s]->ss->d_words + lo,
-                                                    bs[s]->ss->dev, len * 8, st);
-            if (e != hipSuccess) {
-                (void)hipFree(tmp);
-                return nb_internal_fail(NB_ERR_HIP, (std::string("hipMemcpyPeerAsync: ") +
-                                                     hipGetErrorString(e)).c_str());
-            }
+    size_t staged = 0;
+    int rc = NB_OK;
+    for (size_t s = 0; s < bs.size() && !rc; ++s) {
+        if ((int)s == o) continue;
+        const int sdev = bs[s]->ss->dev;
+        if (sdev == dev || peer[(size_t)dev * ndev + sdev]) {
+            srcs.push_back(bs[s]->ss->d_words + lo);
+            continue;
         }
-        const int rc = nb_or_merge_device(own->ss->d_words + lo, tmp, len, nsrc, len, st);
-        if (rc) {
-            (void)hipStreamSynchronize(st);
-            (void)hipFree(tmp);
-            return rc;
+        if (!tmp && hipMalloc(&tmp, (bs.size() - 1) * len * 8) != hipSuccess) {
+            rc = nb_internal_fail(NB_ERR_HIP, "hipMalloc of the merge staging buffer failed");
+            break;
         }
+        const hipError_t e = hipMemcpyPeer(tmp + staged * len, dev, bs[s]->ss->d_words + lo, sdev,
+                                           len * 8);  // blocking: complete on return
+        if (e != hipSuccess)
+            rc = nb_internal_fail(NB_ERR_HIP, (std::string("hipMemcpyPeer: ") + hipGetErrorString(e)).c_str());
+        else
+            srcs.push_back(tmp + (staged++) * len);
     }
-    const hipError_t e1 = hipMemcpyAsync(words + lo, own->ss->d_words + lo, len * 8,
-                                         hipMemcpyDeviceToHost, st);
+    if (!rc) rc = nb_internal_or_gather(own->ss->d_words + lo, srcs.data(), (uint32_t)srcs.size(), len, st);
+    hipError_t e1 = hipSuccess;
+    if (!rc) e1 = hipMemcpyAsync(words + lo, own->ss->d_words + lo, len * 8, hipMemcpyDeviceToHost, st);
     const hipError_t e2 = hipStreamSynchronize(st);
     if (tmp) (void)hipFree(tmp);
+    if (rc) return rc;
     SB_HIP(e1);
     SB_HIP(e2);
     return NB_OK;
@@ -398,15 +405,18 @@ extern "C" int nb_build_sharded(const uint8_t *keys, const uint64_t *offsets, ui
     if (nshards <= 0) nshards = count;
     if (n == 0 || k == 0) return NB_OK;
     if (nshards == 1) return nb_build(keys, offsets, key_len, n, m, k, h2_seed, flavor, words, 0);
-    // direct xGMI peer copies where the devices allow them (already-enabled pairs
-    // report an error that is not one; clear it so no later check sees it)
+    // peer access for the merge's in-place reads over xGMI; peer[a * ndev + b] = 1
+    // once device a may read device b's memory (an already-enabled pair reports an
+    // error that is not one; the sticky error is cleared so no later check sees it)
     const int ndev = std::min(nshards, count);
+    std::vector<char> peer((size_t)ndev * ndev, 0);
     for (int a = 0; a < ndev; ++a) {
         (void)hipSetDevice(a);
         for (int b = 0; b < ndev; ++b) {
             int can = 0;
-            if (a != b && hipDeviceCanAccessPeer(&can, a, b) == hipSuccess && can)
-                (void)hipDeviceEnablePeerAccess(b, 0);
+            if (a == b || hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) continue;
+            const hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+            peer[(size_t)a * ndev + b] = e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled;
         }
         (void)hipGetLastError();
     }
@@ -439,7 +449,7 @@ extern "C" int nb_build_sharded(const uint8_t *keys, const uint64_t *offsets, ui
         const uint64_t nw = ((uint64_t)m + 63) / 64;
         rc = run_all([&](int o) {
             const uint64_t lo = nw * (uint64_t)o / nshards, hi = nw * (uint64_t)(o + 1) / nshards;
-            rcs[o] = hi > lo ? merge_slice(bs, o, lo, hi - lo, words) : NB_OK;
+            rcs[o] = hi > lo ? merge_slice(bs, o, lo, hi - lo, words, peer, ndev) : NB_OK;
             if (rcs[o]) msgs[o] = nb_last_error();
         });
     }
