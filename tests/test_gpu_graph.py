@@ -1,0 +1,63 @@
+"""hipGraph capture of the device build (include/nasp_bloom.h: "warm a stream up with
+its largest shape before capturing it into a hipGraph"): the captured bin + tile
+launches replayed on new keys written into the same buffers give the oracle's
+filter, bit-exact, for the fixed-16 and the variable-length paths."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 17027509906831645879
+
+
+@pytest.fixture(scope="module")
+def dev(built):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("var", [False, True])
+def test_build_replayed_from_graph(dev, oracle, var):
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    n, m, k = 500_000, 4_792_530, 7
+    if var:
+        sets = [synth.var_keys(n, seed=synth.SEED + s) for s in range(3)]
+        ot = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    else:
+        sets = [(synth.fixed_keys(n, 16, seed=synth.SEED + s), None) for s in range(3)]
+        ot = None
+    # one key buffer large enough for every set (replays reuse the captured pointers)
+    kt = torch.zeros(max(b.size for b, _ in sets), dtype=torch.uint8, device=dev)
+    words = torch.zeros(nbm.nwords(m), dtype=torch.int64, device=dev)
+    kl = 0 if var else 16
+    st = torch.cuda.Stream(device=dev)
+
+    def load(i):
+        buf, offs = sets[i]
+        kt[:buf.size].copy_(torch.from_numpy(buf))
+        if var:
+            ot.copy_(torch.from_numpy(offs.view(np.int64)))
+
+    def build():
+        nbm.build_device(kt, ot, kl, n, m, k, SEED, 0, words, stream=st, overwrite=True)
+
+    load(0)
+    torch.cuda.synchronize()
+    with torch.cuda.stream(st):
+        build()  # warm-up: sizes the stream's workspace
+    st.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        build()
+    for i in (1, 2, 0):
+        load(i)
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        buf, offs = sets[i]
+        want = oracle.build(0, buf, offs, kl, n, m, k, SEED)
+        np.testing.assert_array_equal(words.cpu().numpy().view(np.uint64), want)
