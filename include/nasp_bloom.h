@@ -86,10 +86,10 @@ int nb_build(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uin
 /* Single-process multi-GPU nb_build (the C++ host's form of the cooperative C5
  * build, §8(e)): keys split into `nshards` contiguous ranges (<= 0: one per visible
  * device), shard s built on device s % device_count by its own streaming builder
- * and host thread; the partial filters are OR-merged slice-wise -- owner o pulls
- * word slice o of every other partial over xGMI (peer copies), ORs them in
- * (nb_or_merge_device) and downloads its slice into `words`.  Same result and
- * OR-accumulate semantics as nb_build. */
+ * and host thread; the partial filters are OR-merged slice-wise -- owner o ORs
+ * word slice o of every other partial into its own, read in place (over xGMI
+ * with peer access), and downloads its slice into `words`.  Same result and
+ * OR-accumulate semantics as nb_build; at most 64 shards are used. */
 int nb_build_sharded(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                      uint32_t m, uint32_t k, uint64_t h2_seed, int flavor, uint64_t *words,
                      int nshards);

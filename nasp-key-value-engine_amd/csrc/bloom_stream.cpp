@@ -35,6 +35,7 @@ constexpr size_t kChunkBytes = size_t(16) << 20;  // key bytes per chunk
 constexpr size_t kChunkKeys = size_t(1) << 20;    // keys per chunk
 constexpr size_t kSlack = 32;                     // aligned-read slack past a chunk
 constexpr int kSlots = 3;
+constexpr int kMaxShards = 64;  // nb_build_sharded: shards (= host threads) used at most
 
 #define SB_HIP(expr)                                                                     \
     do {                                                                                 \
@@ -403,6 +404,9 @@ extern "C" int nb_build_sharded(const uint8_t *keys, const uint64_t *offsets, ui
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
         return nb_internal_fail(NB_ERR_NODEV, "no HIP device visible");
     if (nshards <= 0) nshards = count;
+    // the filter does not depend on the split: more shards than this only cost
+    // threads and pinned chunk rings
+    nshards = std::min(nshards, kMaxShards);
     if (n == 0 || k == 0) return NB_OK;
     if (nshards == 1) return nb_build(keys, offsets, key_len, n, m, k, h2_seed, flavor, words, 0);
     // peer access for the merge's in-place reads over xGMI; peer[a * ndev + b] = 1
