@@ -36,6 +36,17 @@ def test_no_device_is_reported_not_faked(built):
         pytest.skip("GPU present")
     h = nasp_bloom.lib()
     assert h.nb_device_count() == 0
+    # every building entry point fails loudly (NB_ERR_NODEV), none falls back to the CPU
+    import numpy as np
+    keys = np.zeros(160, np.uint8)
+    words = np.zeros(nasp_bloom.nwords(1000), np.uint64)
+    for call in (lambda: nasp_bloom.build_host(keys, None, 16, 10, 1000, 7, 1, 0, words),
+                 lambda: nasp_bloom.build_host_sharded(keys, None, 16, 10, 1000, 7, 1, 0, words, 2),
+                 lambda: nasp_bloom.probe_host(keys, None, 16, 10, 1000, 7, 1, 0, words),
+                 lambda: nasp_bloom.Builder(1000, 7, 1, 0)):
+        with pytest.raises(nasp_bloom.NaspBloomError, match="device"):
+            call()
+    assert not words.any()
 
 
 def test_formulas_and_seed(built, golden):
