@@ -431,6 +431,44 @@ def test_c3_full_size_properties(dev, oracle):
     assert 0.45 < fill < 0.55
 
 
+def test_c5_full_size_properties(dev, oracle):
+    """C5 at its full size on one GPU: 1B x 32 B keys, k = 10, m = 2^32 - 1 (the
+    two-level path in five 200M-key passes).  (1) OR of 4 shard builds == whole
+    build, (2) every key probes positive, (3) the oracle's filter of the first 1M
+    keys is contained in the full filter, (4) fill matches 1 - exp(-kn/m)."""
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    w = synth.C5
+    g = torch.Generator(device=dev).manual_seed(synth.SEED)
+    kt = torch.randint(0, 256, (w.n * w.key_len,), dtype=torch.uint8, device=dev, generator=g)
+    nw = nbm.nwords(w.m)
+    full = torch.zeros(nw, dtype=torch.int64, device=dev)
+    nbm.build_device(kt, None, w.key_len, w.n, w.m, w.k, SEED, 0, full, overwrite=True)
+    parts = torch.zeros(nw, dtype=torch.int64, device=dev)
+    q = w.n // 4
+    for s in range(4):
+        e = w.n if s == 3 else (s + 1) * q
+        nbm.build_device(kt[s * q * w.key_len:], None, w.key_len, e - s * q, w.m, w.k, SEED, 0,
+                         parts)
+    torch.cuda.synchronize()
+    assert torch.equal(full, parts)
+    del parts
+    out = torch.zeros(w.n, dtype=torch.uint8, device=dev)
+    nbm.probe_device(kt, None, w.key_len, w.n, w.m, w.k, SEED, 0, full, out)
+    torch.cuda.synchronize()
+    assert int(out.min()) == 1
+    del out
+    n_sub = 1_000_000
+    sub_keys = kt[:n_sub * w.key_len].cpu().numpy()
+    fh = full.cpu().numpy().view(np.uint64)
+    sub = oracle.build(0, sub_keys, None, w.key_len, n_sub, w.m, w.k, SEED)
+    assert not (sub & ~fh).any()
+    fill = float(np.bitwise_count(fh).sum(dtype=np.int64)) / w.m
+    expect = 1.0 - np.exp(-w.k * w.n / w.m)  # 0.903
+    assert abs(fill - expect) < 0.005
+
+
 # --------------------------------------------------------- host entry points --
 
 def test_host_entry_points(dev, oracle):
