@@ -431,6 +431,40 @@ def test_c3_full_size_properties(dev, oracle):
     assert 0.45 < fill < 0.55
 
 
+def test_c4_full_size_properties(dev, oracle):
+    """C4's per-GPU shard at full size: 100M x 16 B keys, k = 7, m = 958 505 838
+    (2^19-bit tiles, 32-bit bucket entries): shard-OR identity, no false negatives,
+    the oracle's filter of the first 1M keys contained, fill ~ 50 %."""
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    w = synth.C4
+    g = torch.Generator(device=dev).manual_seed(synth.SEED + 4)
+    kt = torch.randint(0, 256, (w.n * 16,), dtype=torch.uint8, device=dev, generator=g)
+    nw = nbm.nwords(w.m)
+    full = torch.zeros(nw, dtype=torch.int64, device=dev)
+    nbm.build_device(kt, None, 16, w.n, w.m, w.k, SEED, 0, full, overwrite=True)
+    parts = torch.zeros(nw, dtype=torch.int64, device=dev)
+    q = w.n // 3
+    for s in range(3):
+        e = w.n if s == 2 else (s + 1) * q
+        nbm.build_device(kt[s * q * 16:], None, 16, e - s * q, w.m, w.k, SEED, 0, parts)
+    torch.cuda.synchronize()
+    assert torch.equal(full, parts)
+    del parts
+    out = torch.zeros(w.n, dtype=torch.uint8, device=dev)
+    nbm.probe_device(kt, None, 16, w.n, w.m, w.k, SEED, 0, full, out)
+    torch.cuda.synchronize()
+    assert int(out.min()) == 1
+    del out
+    n_sub = 1_000_000
+    fh = full.cpu().numpy().view(np.uint64)
+    sub = oracle.build(0, kt[:n_sub * 16].cpu().numpy(), None, 16, n_sub, w.m, w.k, SEED)
+    assert not (sub & ~fh).any()
+    fill = float(np.bitwise_count(fh).sum(dtype=np.int64)) / w.m
+    assert abs(fill - (1.0 - np.exp(-w.k * w.n / w.m))) < 0.005
+
+
 def test_c5_full_size_properties(dev, oracle):
     """C5 at its full size on one GPU: 1B x 32 B keys, k = 10, m = 2^32 - 1 (the
     two-level path in five 200M-key passes).  (1) OR of 4 shard builds == whole
