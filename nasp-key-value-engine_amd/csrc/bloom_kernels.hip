@@ -1086,13 +1086,18 @@ uint32_t env_u32(const char *name, uint32_t dflt) {
 // Tile size policy (measured, tools/ubench_tiled.hip): 2^16-bit tiles with 16-bit
 // bucket entries while that needs <= 2048 tiles (m <= 2^27, e.g. C2); smaller
 // tiles for small m (>= ~1024 tiles, 2^12 bits minimum); above 2^27 bits the
-// smallest ts giving <= 2048 tiles (C3/C4: ts = 19), up to 2^20-bit tiles
-// (<= 4096 tiles at m = 2^32 - 1, C5) with 32-bit entries.
+// entries are 32-bit whatever the tile size, so the largest tiles (up to 2^20
+// bits) that still leave >= 512 tile blocks: fewer tiles make a block's runs
+// longer (fewer reservation atomics and L2 write requests).  C3/C4: ts = 20,
+// T = 915 (C4 2.31 -> 1.99 ms, C3 3.68 -> 3.35 ms vs ts = 19, T = 1 829);
+// C5: ts = 20, 4 096 fine tiles.
 TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     TileCfg tc;
     uint32_t ts = 12;
     while (ts < 16 && ((uint64_t)m >> (ts + 1)) >= 1024) ++ts;
     while (ts < 20 && (((uint64_t)m + (1ull << ts) - 1) >> ts) > 2048) ++ts;
+    if (ts > 16)
+        while (ts < 20 && (((uint64_t)m + (2ull << ts) - 1) >> (ts + 1)) >= 512) ++ts;
     ts = std::min<uint32_t>(std::max<uint32_t>(env_u32("NB_TILE_BITS", ts), 12), 20);
     tc.ts = ts;
     tc.T = (uint32_t)(((uint64_t)m + (1ull << ts) - 1) >> ts);
