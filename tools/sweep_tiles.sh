@@ -9,6 +9,7 @@ run() {  # name workload env...
     > gpurun_out/sweep/$name.json 2> gpurun_out/sweep/$name.err || { echo "$name failed"; return 1; }
   python -c "import json,sys; d=json.loads(open('gpurun_out/sweep/$name.json').read().strip().splitlines()[-1]); print('$name', d['value'], d['roofline']['kernel_ms'])"
 }
-run c4_ts19 c4 NB_X=0 && run c4_ts20 c4 NB_TILE_BITS=20 && run c4_g4 c4 NB_SHARDS=4 && run c4_ts19b c4 NB_X=0 \
-&& run c3_ts19 c3 NB_X=0 && run c3_ts20 c3 NB_TILE_BITS=20 \
-&& run c2_ts16 c2 NB_X=0 && run c2_ts17 c2 NB_TILE_BITS=17 && run c2_g4 c2 NB_SHARDS=4 && run c2_ts16b c2 NB_X=0
+run c2_g8 c2 NB_SHARDS=8 && run c2_g16 c2 NB_SHARDS=16 && run c2_g12 c2 NB_SHARDS=12 && run c2_g8b c2 NB_SHARDS=8 && run c2_g16b c2 NB_SHARDS=16 \
+&& run c4_g8 c4 NB_SHARDS=8 && run c4_g16 c4 NB_SHARDS=16 && run c4_g8b c4 NB_SHARDS=8 \
+&& run c3_g8 c3 NB_SHARDS=8 && run c3_g16 c3 NB_SHARDS=16 \
+&& run c5_g8 c5 NB_SHARDS=8 && run c5_g16 c5 NB_SHARDS=16
