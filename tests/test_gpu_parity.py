@@ -308,6 +308,39 @@ def test_tiled_bucket_overflow_spill(dev, oracle, monkeypatch):
     np.testing.assert_array_equal(got, want)
 
 
+# Tile policy boundaries (bloom_kernels.hip choose_tiles): u16 entries up to
+# m = 2^27 (ts 16, T 2048); above it 32-bit entries with the largest tiles that
+# leave >= 512 of them -- 2^27+1 -> ts 18 / T 513, 2^28-1 -> ts 19 / T 512,
+# C3/C4's m -> ts 20 / T 915, 2^31-1 -> ts 20 / T 2048 (last single-level m),
+# 2^31+1 -> two-level.  Ragged last tiles included.
+@pytest.mark.parametrize("m", [2**27, 2**27 + 1, 2**28 - 1, 300_000_001, 958_505_838,
+                               2**31 - 1, 2**31 + 1])
+def test_tile_policy_boundaries(dev, oracle, m, monkeypatch):
+    from nasp_bloom import synth
+    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    n = 300_000
+    buf = synth.fixed_keys(n, 16)
+    got = dev_build(dev, buf, None, 16, n, m, 7, SEED)
+    want = oracle.build(0, buf, None, 16, n, m, 7, SEED)
+    np.testing.assert_array_equal(got, want)
+    vbuf, voffs = synth.var_keys(n, 8, 64)
+    got = dev_build(dev, vbuf, voffs, 0, n, m, 7, SEED, flavor=1)
+    want = oracle.build(1, vbuf, voffs, 0, n, m, 7, SEED)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_tiled_overflow_spill_large_tiles(dev, oracle, monkeypatch):
+    """The spill path with 32-bit entries and 2^20-bit tiles (C4's m)."""
+    from nasp_bloom import synth
+    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    n = 400_000
+    buf = np.zeros(n * 16 + 16, np.uint8)
+    buf[: 16 * 1000] = synth.fixed_keys(1000, 16)[: 16 * 1000]
+    got = dev_build(dev, buf, None, 16, n, 958_505_838, 7, SEED)
+    want = oracle.build(0, buf, None, 16, n, 958_505_838, 7, SEED)
+    np.testing.assert_array_equal(got, want)
+
+
 @pytest.mark.parametrize("two_level", ["1", "0"])
 @pytest.mark.parametrize("chunk", ["0", "300000"])
 def test_two_level_build_large_m(dev, oracle, two_level, chunk, monkeypatch):
