@@ -358,7 +358,11 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     } else if (t0 < T) {
         h0 = cnt[t0];
     }
-    const uint32_t local = h0 + h1;
+    // packed entries (ENTRY = u64, 3 in-tile offsets per word): every run takes a
+    // whole number of words, its 1-2 pad slots hold copies of its first entry
+    constexpr bool PACK = sizeof(ENTRY) == 8;
+    auto slots = [](uint32_t c) { return PACK ? (c + 2) / 3 * 3 : c; };
+    const uint32_t local = slots(h0) + slots(h1);
     const uint32_t incl = wave_inclusive_scan(local);
     if (lane == 63) wave_sums[wid] = incl;
     __syncthreads();
@@ -369,7 +373,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
         if (lane == kWaves - 1) wave_sums[kWaves] = wi;
     }
     __syncthreads();
-    const uint32_t st0 = wave_sums[wid] + incl - local, st1 = st0 + h0;
+    const uint32_t st0 = wave_sums[wid] + incl - local, st1 = st0 + slots(h0);
     const uint32_t total = wave_sums[kWaves];
     const uint32_t shard = blockIdx.x % tc.G;
     uint32_t *cur = sc.gcur + (size_t)shard * T;
@@ -378,8 +382,9 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     // atomic line is a memory-side request (WRITE_SIZE measured 57 vs 30 MB/build)
     const uint32_t ta = tid, tb = tid + NT;
     const uint32_t ha = ta < T ? cnt[ta] : 0u, hb = tb < T ? cnt[tb] : 0u;
-    const uint32_t ga = ha ? atomicAdd(&cur[ta], ha) : 0u;
-    const uint32_t gb = hb ? atomicAdd(&cur[tb], hb) : 0u;
+    const uint32_t ua = PACK ? (ha + 2) / 3 : ha, ub = PACK ? (hb + 2) / 3 : hb;  // bucket units
+    const uint32_t ga = ua ? atomicAdd(&cur[ta], ua) : 0u;
+    const uint32_t gb = ub ? atomicAdd(&cur[tb], ub) : 0u;
     if (t0 < T) S4[t0] = sort_b + 4 * st0;  // (S4 + t0 is 8-byte aligned only for even T)
     if (t0 + 1 < T) S4[t0 + 1] = sort_b + 4 * st1;
     __syncthreads();
@@ -395,20 +400,27 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
                         ridx[p][j];
         }
     }
-    const int ovf = ((uint64_t)ga + ha > tc.cap) | ((uint64_t)gb + hb > tc.cap);
+    const int ovf = ((uint64_t)ga + ua > tc.cap) | ((uint64_t)gb + ub > tc.cap);
     const bool any_ovf = __syncthreads_or(ovf) != 0;  // cnt and S4 are dead now
     // run table: first-entry index minus the run's local start (wrapping u32), in
     // bytes when the buckets fit 32-bit offsets; limits over S4 on overflow
     const bool b32 = (uint64_t)T * tc.G * tc.cap * sizeof(ENTRY) <= 0xFFFFFFFFull;
     const uint32_t esz = (b32 && !any_ovf) ? (uint32_t)sizeof(ENTRY) : 1u;
-    auto run_entry = [&](uint32_t t, uint32_t g) {
-        const uint32_t st = (S4[t] - sort_b) / 4;
+    // (packed: st and the table in words; the pad slots are filled here -- the
+    // placement is complete, and nothing else touches the sort area until phase 4)
+    auto run_entry = [&](uint32_t t, uint32_t g, uint32_t h) {
+        uint32_t st = (S4[t] - sort_b) / 4;
+        if (PACK) {
+            uint32_t *run = lds + sort_off_words + st;
+            for (uint32_t r = h; r < slots(h); ++r) run[r] = run[0];
+            st /= 3;
+        }
         cnt[t] = ((t * tc.G + shard) * tc.cap + g - st) * esz;
         return st;
     };
     uint32_t sa = 0, sbb = 0;
-    if (ta < T) sa = run_entry(ta, ga);
-    if (tb < T) sbb = run_entry(tb, gb);
+    if (ta < T) sa = run_entry(ta, ga, ha);
+    if (tb < T) sbb = run_entry(tb, gb, hb);
     if (any_ovf) {
         __syncthreads();  // every thread has read S4 before limits go over it
         if (ta < T) S4[ta] = sa + (ga < tc.cap ? tc.cap - ga : 0u);
@@ -419,6 +431,50 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     // ---- phase 4: coalesced write-out, four independent entries per lane per step
     const uint32_t *sorted = lds + sort_off_words;
     const uint32_t *GX = cnt;
+    if constexpr (PACK) {
+        // word q of the block = slots 3q..3q+2 (one run, tile of the first slot)
+        const uint32_t words = total / 3, msk = (1u << tc.ts) - 1;
+        auto word_at = [&](uint32_t q, uint32_t *t) {
+            const uint32_t a = sorted[3 * q], b = sorted[3 * q + 1], c = sorted[3 * q + 2];
+            *t = a >> tc.ts;
+            return (uint64_t)(a & msk) | ((uint64_t)(b & msk) << 21) | ((uint64_t)(c & msk) << 42);
+        };
+        if (!any_ovf && b32) {
+            char *bb = reinterpret_cast<char *>(buckets);
+            uint32_t q = tid;
+            for (; q + NT < words; q += 2 * NT) {
+                uint32_t t[2];
+                uint64_t w[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) w[u] = word_at(q + u * NT, &t[u]);
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    *reinterpret_cast<uint64_t *>(bb + (GX[t[u]] + (q + u * NT) * 8u)) = w[u];
+            }
+            for (; q < words; q += NT) {
+                uint32_t t;
+                const uint64_t w = word_at(q, &t);
+                *reinterpret_cast<uint64_t *>(bb + (GX[t] + q * 8u)) = w;
+            }
+        } else {
+            uint64_t *bw = reinterpret_cast<uint64_t *>(buckets);
+            for (uint32_t q = tid; q < words; q += NT) {
+                uint32_t t;
+                const uint64_t w = word_at(q, &t);
+                if (!any_ovf || q < S4[t]) {
+                    bw[(uint32_t)(GX[t] + q)] = w;
+                } else {  // past the bucket's capacity: the three entries to the spill bitmap
+                    for (uint32_t r = 0; r < 3; ++r) {
+                        const uint32_t v = sorted[3 * q + r];
+                        __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31),
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        sc.spill_flag[v >> tc.fts] = 1u;
+                    }
+                }
+            }
+        }
+        return;
+    }
     if (!any_ovf && b32) {
         char *bb = reinterpret_cast<char *>(buckets);
         uint32_t j = tid;
@@ -617,7 +673,8 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     }
     __syncthreads();
     if (NB_DIAG_STOP(1)) return;
-    if (NB_TWO_TILE && KR > 0 && T <= 2 * NT) {  // block-uniform: the common case (C2: T = 1 463)
+    if (sizeof(ENTRY) == 8 || (NB_TWO_TILE && KR > 0 && T <= 2 * NT)) {  // block-uniform:
+        // the common case (C2: T = 1 463); packed entries (host-checked T <= 2 NT, KR > 0) always
         bin_tail_two_tiles<NT, KPT, kR>(lds, bin_sort_offset_words(T), tc, sc, buckets, base, n,
                                         c.k, ridx, rank);
         return;
@@ -886,6 +943,9 @@ __global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
         if (sizeof(ENTRY) == 2) {
             orv(q.x & 0xffff); orv(q.x >> 16); orv(q.y & 0xffff); orv(q.y >> 16);
             orv(q.z & 0xffff); orv(q.z >> 16); orv(q.w & 0xffff); orv(q.w >> 16);
+        } else if (sizeof(ENTRY) == 8) {  // two words of three 21-bit offsets
+            orv(q.x); orv((q.x >> 21) | (q.y << 11)); orv(q.y >> 10);
+            orv(q.z); orv((q.z >> 21) | (q.w << 11)); orv(q.w >> 10);
         } else {
             orv(q.x); orv(q.y); orv(q.z); orv(q.w);
         }
@@ -912,7 +972,14 @@ __global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
     if (tid < tc.G) {  // each shard's tail (< kPerVec entries)
         const uint32_t cnt = shard_cnt[tid];
         const ENTRY *e = tile_base + (size_t)tid * tc.cap;
-        for (uint32_t r = cnt / kPerVec * kPerVec; r < cnt; ++r) orv(e[r]);
+        for (uint32_t r = cnt / kPerVec * kPerVec; r < cnt; ++r) {
+            const uint64_t x = (uint64_t)e[r];
+            orv((uint32_t)x);
+            if (sizeof(ENTRY) == 8) {
+                orv((uint32_t)(x >> 21));
+                orv((uint32_t)(x >> 42));
+            }
+        }
     }
     const uint64_t w0 = (uint64_t)t << (tc.ts - 6);
     const uint32_t tile_words64 = tile_words32 / 2;
@@ -1175,6 +1242,7 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     if ((rc = ws_reserve(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * sizeof(ENTRY), &sc)))
         return rc;
     size_t sort_bytes = kpb * c.k * 4;
+    if (sizeof(ENTRY) == 8) sort_bytes += (size_t)tc.T * 8;  // <= 2 pad slots per run
     if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(NT));
     const size_t bin_lds = (size_t)bin_sort_offset_words(tc.T) * 4 + sort_bytes;
     const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
@@ -1271,6 +1339,21 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
     if (tc.ts <= 16 && env_u32("NB_ENTRY32", 0) == 0)
         return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint16_t, NT, STAGE, KR>(
             keys, offsets, key_len, n, c, words, overwrite, st, chunk, tc);
+    if constexpr (KR > 0) {
+        // 17-20-bit in-tile offsets: three per 64-bit bucket word (the two-tile
+        // tail pads each block-local run to a multiple of 3 with copies of its
+        // first entry).  Capacity in words: the entries' plus <= 2 pads per run,
+        // i.e. per block of the shard.
+        if (tc.ts <= 20 && tc.T <= 2u * NT && NB_TWO_TILE && env_u32("NB_PACK", 1) != 0) {
+            const uint64_t nblk = (chunk + kpb - 1) / kpb;
+            const uint64_t bps = (nblk + tc.G - 1) / tc.G;
+            const uint64_t capw = ((uint64_t)tc.cap + 2 * bps + 2) / 3;
+            TileCfg tp = tc;
+            tp.cap = (uint32_t)std::min<uint64_t>((capw + 7) & ~7ull, 0xFFFFFFC0ull);
+            return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint64_t, NT, STAGE, KR>(
+                keys, offsets, key_len, n, c, words, overwrite, st, chunk, tp);
+        }
+    }
     return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint32_t, NT, STAGE, KR>(
         keys, offsets, key_len, n, c, words, overwrite, st, chunk, tc);
 }
