@@ -840,12 +840,18 @@ constexpr int kRebinThreads = 1024;
 constexpr int kRebinEPT = 16;        // entries per thread
 constexpr uint32_t kRebinSpan = kRebinThreads * kRebinEPT;
 
+// PACK: fine entries three per 64-bit word (runs padded to a multiple of 3 slots
+// with copies of their first entry, as in bin_tail_two_tiles); capacities,
+// cursors and the run table in words.
+template <bool PACK>
 __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
     TileCfg t1, TileCfg t2, TileScratch sc1, TileScratch sc2, const uint32_t *__restrict__ b1,
-    uint32_t *__restrict__ b2) {
+    void *__restrict__ b2v) {
     __shared__ uint32_t v0[kShards + 1];
     __shared__ uint32_t fcnt[kSuperFine], fS[kSuperFine], fGX[kSuperFine], flim[kSuperFine];
+    __shared__ uint32_t slot_total;
     __shared__ int any_ovf;
+    uint32_t *b2 = reinterpret_cast<uint32_t *>(b2v);
     extern __shared__ uint32_t sorted[];  // [kRebinSpan]
     const uint32_t tid = threadIdx.x, s = blockIdx.y;
     if (tid == 0) {
@@ -881,14 +887,17 @@ __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
     __syncthreads();
     if (tid < kSuperFine) {  // wave 0: scan the 64 counts, reserve the 64 runs
         const uint32_t c = fcnt[tid];
-        const uint32_t st = wave_inclusive_scan(c) - c;
+        const uint32_t sl = PACK ? (c + 2) / 3 * 3 : c, u = PACK ? sl / 3 : c;
+        const uint32_t incl = wave_inclusive_scan(sl), st = incl - sl;
+        if (tid == kSuperFine - 1) slot_total = incl;
         const uint32_t t = fbase + tid;
         const uint32_t shard = (blockIdx.y * gridDim.x + blockIdx.x) % t2.G;
-        const uint32_t gr = c ? atomicAdd(&sc2.gcur[(size_t)shard * t2.T + t], c) : 0u;
+        const uint32_t gr = u ? atomicAdd(&sc2.gcur[(size_t)shard * t2.T + t], u) : 0u;
+        const uint32_t stu = PACK ? st / 3 : st;
         fS[tid] = st;
-        fGX[tid] = (t * t2.G + shard) * t2.cap + gr - st;
-        flim[tid] = st + (gr < t2.cap ? t2.cap - gr : 0u);
-        if ((uint64_t)gr + c > t2.cap) any_ovf = 1;
+        fGX[tid] = (t * t2.G + shard) * t2.cap + gr - stu;
+        flim[tid] = stu + (gr < t2.cap ? t2.cap - gr : 0u);
+        if ((uint64_t)gr + u > t2.cap) any_ovf = 1;
     }
     __syncthreads();
 #pragma unroll
@@ -896,6 +905,31 @@ __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
         if (tid + u * kRebinThreads < cnt) sorted[fS[(v[u] >> t2.ts) - fbase] + r[u]] = v[u];
     __syncthreads();
     const bool ovf = any_ovf != 0;
+    if constexpr (PACK) {
+        if (tid < kSuperFine) {  // pad slots: copies of the run's first entry
+            const uint32_t c = fcnt[tid], st = fS[tid];
+            for (uint32_t q = c; q < (c + 2) / 3 * 3; ++q) sorted[st + q] = sorted[st];
+        }
+        __syncthreads();
+        uint64_t *bw = reinterpret_cast<uint64_t *>(b2v);
+        const uint32_t words = slot_total / 3, msk = (1u << t2.ts) - 1;
+        for (uint32_t q = tid; q < words; q += kRebinThreads) {
+            const uint32_t a = sorted[3 * q], b = sorted[3 * q + 1], c = sorted[3 * q + 2];
+            const uint32_t f = (a >> t2.ts) - fbase;
+            if (!ovf || q < flim[f]) {
+                bw[fGX[f] + q] = (uint64_t)(a & msk) | ((uint64_t)(b & msk) << 21) |
+                                 ((uint64_t)(c & msk) << 42);
+            } else {
+                for (uint32_t rr = 0; rr < 3; ++rr) {
+                    const uint32_t x = sorted[3 * q + rr];
+                    __hip_atomic_fetch_or(sc2.spill32 + (x >> 5), 1u << (x & 31), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                    sc2.spill_flag[x >> t2.ts] = 1u;
+                }
+            }
+        }
+        return;
+    }
     for (uint32_t j = tid; j < cnt; j += kRebinThreads) {
         const uint32_t x = sorted[j], f = (x >> t2.ts) - fbase;
         if (!ovf || j < flim[f]) {
@@ -1268,6 +1302,13 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     return NB_OK;
 }
 
+// The tile kernel for an entry type, as a type-erased launch target.
+template <typename ENTRY, bool OVERWRITE>
+void (*tile_kernel_of())(TileCfg, TileScratch, const void *, uint64_t *, uint64_t) {
+    return reinterpret_cast<void (*)(TileCfg, TileScratch, const void *, uint64_t *, uint64_t)>(
+        bloom_tile_or_kernel<ENTRY, OVERWRITE>);
+}
+
 // The two-level build (see bloom_rebin_kernel): per chunk, the bin kernel into
 // super tiles, the re-bin into fine tiles, the tile kernel on the fine tiles.
 template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR>
@@ -1279,28 +1320,39 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
     TileScratch sc;
     int rc;
     if ((rc = get_ws(st, &ws))) return rc;
+    const uint32_t rebin_x = (uint32_t)(((uint64_t)t1.cap * t1.G + kRebinSpan - 1) / kRebinSpan);
+    // fine entries packed three per word (2^ts2 <= 2^21): capacity in words, the
+    // entries' plus <= 2 pad slots per re-bin block of the shard
+    const bool pack = t2.ts <= 20 && env_u32("NB_PACK", 1) != 0;
+    TileCfg t2p = t2;
+    if (pack) {
+        const uint64_t bps = ((uint64_t)rebin_x + t2.G - 1) / t2.G;
+        const uint64_t capw = ((uint64_t)t2.cap + 2 * bps + 2) / 3;
+        t2p.cap = (uint32_t)std::min<uint64_t>((capw + 7) & ~7ull, 0xFFFFFFC0ull);
+    }
+    const size_t e2 = pack ? 8 : 4;
     if ((rc = ws_reserve(*ws, c.fm.m, (size_t)t1.T * t1.G * t1.cap * 4, &sc,
-                         (size_t)t2.T * t2.G * t2.cap * 4)))
+                         (size_t)t2p.T * t2p.G * t2p.cap * e2)))
         return rc;
     TileScratch sc1 = sc;
     sc1.gcur = super_cursors(*ws);
     size_t sort_bytes = kpb * c.k * 4;
     if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(NT));
     const size_t bin_lds = (size_t)bin_sort_offset_words(t1.T) * 4 + sort_bytes;
-    const size_t rebin_lds = (size_t)kRebinSpan * 4;
+    const size_t rebin_lds = ((size_t)kRebinSpan + 2 * kSuperFine) * 4;
     const size_t tile_lds = ((size_t)1 << (t2.ts - 3)) + (2 * kShards + 1) * 4;
     auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, uint32_t, NT, STAGE, KR>;
-    auto tile_ow = bloom_tile_or_kernel<uint32_t, true>;
-    auto tile_or = bloom_tile_or_kernel<uint32_t, false>;
+    auto rebin = pack ? bloom_rebin_kernel<true> : bloom_rebin_kernel<false>;
+    auto tile_ow = pack ? tile_kernel_of<uint64_t, true>() : tile_kernel_of<uint32_t, true>();
+    auto tile_or = pack ? tile_kernel_of<uint64_t, false>() : tile_kernel_of<uint32_t, false>();
     if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(tile_ow, tile_lds)) ||
         (rc = allow_lds(tile_or, tile_lds)))
         return rc;
-    NB_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(bloom_rebin_kernel),
+    NB_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(rebin),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rebin_lds));
     const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
     uint32_t *b1 = reinterpret_cast<uint32_t *>(ws->buckets);
-    uint32_t *b2 = reinterpret_cast<uint32_t *>(ws->buckets2);
-    const uint32_t rebin_x = (uint32_t)(((uint64_t)t1.cap * t1.G + kRebinSpan - 1) / kRebinSpan);
+    void *b2 = ws->buckets2;
     for (uint64_t done = 0; done < n; done += chunk) {
         const uint64_t cn = std::min(chunk, n - done);
         const uint8_t *ck = offsets ? keys : keys + done * key_len;
@@ -1308,12 +1360,12 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
         hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st, ck,
                            co, key_len, cn, c, t1, sc1, b1);
         NB_HIP(hipGetLastError());
-        hipLaunchKernelGGL(bloom_rebin_kernel, dim3(rebin_x, t1.T), dim3(kRebinThreads), rebin_lds,
-                           st, t1, t2, sc1, sc, b1, b2);
+        hipLaunchKernelGGL(rebin, dim3(rebin_x, t1.T), dim3(kRebinThreads), rebin_lds,
+                           st, t1, t2p, sc1, sc, b1, b2);
         NB_HIP(hipGetLastError());
         NB_HIP(hipMemsetAsync(sc1.gcur, 0, (size_t)t1.G * t1.T * 4, st));  // keep them zero
         hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(t2.T),
-                           dim3(kTileThreads), tile_lds, st, t2, sc, b2, words, nwords);
+                           dim3(kTileThreads), tile_lds, st, t2p, sc, b2, words, nwords);
         NB_HIP(hipGetLastError());
     }
     return NB_OK;
