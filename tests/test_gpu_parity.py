@@ -329,6 +329,31 @@ def test_tile_policy_boundaries(dev, oracle, m, monkeypatch):
     np.testing.assert_array_equal(got, want)
 
 
+def test_packed_entries_past_4gib(dev, monkeypatch):
+    """Packed bucket words past 4 GiB of buckets (word-indexed write-out): 120M
+    keys x k = 16 into m = 2^31 - 1 (2^20-bit tiles, 1.92G entries = 5.1 GB of
+    packed words in one chunk) must give the same filter as 32-bit entries
+    (NB_PACK=0, checked against the oracle elsewhere), with no false negatives."""
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    n, m, k = 120_000_000, 2**31 - 1, 16
+    kt = t_u8(synth.fixed_keys(n, 16), dev)
+    out = []
+    for pack in ("1", "0"):
+        monkeypatch.setenv("NB_PACK", pack)
+        wt = torch.zeros(nbm.nwords(m), dtype=torch.int64, device=dev)
+        nbm.build_device(kt, None, 16, n, m, k, SEED, 0, wt)
+        torch.cuda.synchronize()
+        out.append(wt)
+    assert torch.equal(out[0], out[1])
+    res = torch.empty(n, dtype=torch.uint8, device=dev)
+    nbm.probe_device(kt, None, 16, n, m, k, SEED, 0, out[0], res)
+    torch.cuda.synchronize()
+    assert int(res.min()) == 1
+
+
 def test_tiled_overflow_spill_large_tiles(dev, oracle, monkeypatch):
     """The spill path with 32-bit entries and 2^20-bit tiles (C4's m)."""
     from nasp_bloom import synth
