@@ -1197,8 +1197,17 @@ TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     uint32_t ts = 12;
     while (ts < 16 && ((uint64_t)m >> (ts + 1)) >= 1024) ++ts;
     while (ts < 20 && (((uint64_t)m + (1ull << ts) - 1) >> ts) > 2048) ++ts;
-    if (ts > 16)
-        while (ts < 20 && (((uint64_t)m + (2ull << ts) - 1) >> (ts + 1)) >= 512) ++ts;
+    auto tiles = [m](uint32_t s) { return ((uint64_t)m + (1ull << s) - 1) >> s; };
+    if (m >= (1u << 24) && k <= 16 && env_u32("NB_PACK", 1) != 0) {
+        // packed 21-bit entries (k <= 16: the rank-mode tail): larger tiles, down
+        // to ~160 of them -- C2 at 2^19-bit tiles (T = 183) 0.162-0.167 ms vs
+        // 0.171-0.176 with u16 entries at 2^16 bits (3 interleaved repeats,
+        // tools/sweep_c2.sh): a third more entry bytes, runs 8x longer
+        ts = std::max<uint32_t>(ts, 17);
+        while (ts < 20 && tiles(ts + 1) >= 160) ++ts;
+    } else if (ts > 16) {
+        while (ts < 20 && tiles(ts + 1) >= 512) ++ts;
+    }
     ts = std::min<uint32_t>(std::max<uint32_t>(env_u32("NB_TILE_BITS", ts), 12), 20);
     tc.ts = ts;
     tc.T = (uint32_t)(((uint64_t)m + (1ull << ts) - 1) >> ts);
@@ -1396,7 +1405,14 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
         // tail pads each block-local run to a multiple of 3 with copies of its
         // first entry).  Capacity in words: the entries' plus <= 2 pads per run,
         // i.e. per block of the shard.
-        if (tc.ts <= 20 && tc.T <= 2u * NT && NB_TWO_TILE && env_u32("NB_PACK", 1) != 0) {
+        // ... only while two bin blocks still fit a CU's LDS with the pad slots (up to
+        // T ~ 1 100: packed C4 at 2^19-bit tiles, T = 1 829, ran 2.47 vs 2.30 ms with
+        // one block per CU)
+        size_t pk_lds = (size_t)kpb * c.k * 4 + (size_t)tc.T * 8;
+        if (STAGE) pk_lds = std::max<size_t>(pk_lds, stage_lds_bytes(NT));
+        pk_lds += (size_t)bin_sort_offset_words(tc.T) * 4;
+        if (tc.ts <= 20 && tc.T <= 2u * NT && NB_TWO_TILE && pk_lds <= 80 * 1024 &&
+            env_u32("NB_PACK", 1) != 0) {
             const uint64_t nblk = (chunk + kpb - 1) / kpb;
             const uint64_t bps = (nblk + tc.G - 1) / tc.G;
             const uint64_t capw = ((uint64_t)tc.cap + 2 * bps + 2) / 3;

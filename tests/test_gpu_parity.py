@@ -311,10 +311,12 @@ def test_tiled_bucket_overflow_spill(dev, oracle, monkeypatch):
 # Tile policy boundaries (bloom_kernels.hip choose_tiles): u16 entries up to
 # m = 2^27 (ts 16, T 2048); above it 32-bit entries with the largest tiles that
 # leave >= 512 of them -- 2^27+1 -> ts 18 / T 513, 2^28-1 -> ts 19 / T 512,
-# C3/C4's m -> ts 20 / T 915, 2^31-1 -> ts 20 / T 2048 (last single-level m),
-# 2^31+1 -> two-level.  Ragged last tiles included.
+# C3/C4's m -> ts 20 / T 915, 2^30+7 -> T 1025 (packed entries: two bin blocks
+# still fit a CU's LDS), 2^31-1 -> ts 20 / T 2048 (32-bit entries: the pad slots
+# would not fit two blocks; last single-level m), 2^31+1 -> two-level.  Ragged
+# last tiles included.
 @pytest.mark.parametrize("m", [2**27, 2**27 + 1, 2**28 - 1, 300_000_001, 958_505_838,
-                               2**31 - 1, 2**31 + 1])
+                               2**30 + 7, 2**31 - 1, 2**31 + 1])
 def test_tile_policy_boundaries(dev, oracle, m, monkeypatch):
     from nasp_bloom import synth
     monkeypatch.setenv("NB_BUILD_PATH", "tiled")
@@ -331,14 +333,14 @@ def test_tile_policy_boundaries(dev, oracle, m, monkeypatch):
 
 def test_packed_entries_past_4gib(dev, monkeypatch):
     """Packed bucket words past 4 GiB of buckets (word-indexed write-out): 120M
-    keys x k = 16 into m = 2^31 - 1 (2^20-bit tiles, 1.92G entries = 5.1 GB of
-    packed words in one chunk) must give the same filter as 32-bit entries
+    keys x k = 16 into m = 900 x 2^20 (900 2^20-bit tiles, packed while two bin
+    blocks fit a CU's LDS; 1.92G entries = 5.1 GB of packed words in one chunk) must give the same filter as 32-bit entries
     (NB_PACK=0, checked against the oracle elsewhere), with no false negatives."""
     import torch
     import nasp_bloom as nbm
     from nasp_bloom import synth
     monkeypatch.setenv("NB_BUILD_PATH", "tiled")
-    n, m, k = 120_000_000, 2**31 - 1, 16
+    n, m, k = 120_000_000, 900 << 20, 16
     kt = t_u8(synth.fixed_keys(n, 16), dev)
     out = []
     for pack in ("1", "0"):
