@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """bench.py -- device-resident Bloom-filter build throughput (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c1]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c4|c2|c3|c1|c5|merkle]
+
+Default workload: C4's per-GPU shard, 100M x 16 B keys, k = 7 (m = 958,505,838):
+the shape the north star's target ("100M x 16B keys at k=7") is quoted on, and
+at N GPUs exactly BASELINE config 4 (one independent SSTable filter per GPU).
 
 One step = one pass of the hot path over one batch: build a fresh filter from
 every key of the batch (hash + index + bit scatter + filter store; the library's
@@ -10,10 +14,13 @@ its own independent filter over its own keys (the compaction fan-out, C4) --
 weak scaling, no data-path collective.  `value` = all keys of all ranks / the
 max-over-ranks time of the K timed steps.
 
-Extra fields: `roofline` (dominant kernel, HIP-event timed on its own stream;
-achieved = algorithmic bytes / average launch time) and, on rank 0 at
-N = 1, `cpu_baseline` (the reference BloomFilter.cpp compiled here, timed on a
-bounded sample of the same workload, 1 core).
+Extra fields: `roofline` (the build call's kernels, HIP-event timed on their own
+stream; achieved = algorithmic bytes / average build time; traffic
+and valu_frac from the committed rocprofv3 PMC summaries of the current kernel
+source) and, on rank 0 at N = 1, `cpu_baseline` (the reference BloomFilter.cpp
+compiled here, timed on a bounded sample of the same workload: 1 pinned core, or
+for C4 8 concurrent builds on 8 pinned cores) and `c2` (BASELINE config 2's
+device-resident rate, the round-1 headline, measured in the same run).
 """
 from __future__ import annotations
 
@@ -155,13 +162,45 @@ def host_path_rate(wl, keys_np, offs_np, key_len, seed, flavor, reps=3):
                    "device build; best of %d" % reps}
     exe = os.path.join(REPO, "nasp-key-value-engine_amd", "build", "sstable_filter_bench")
     if offs_np is None and os.path.exists(exe):
-        r = subprocess.run([exe, str(wl.n), str(key_len), str(reps)], capture_output=True,
-                           text=True, timeout=300)
+        # 10M std::string keys at most (C4's 100M would hold ~5 GB of strings)
+        r = subprocess.run([exe, str(min(wl.n, 10_000_000)), str(key_len), str(reps)],
+                           capture_output=True, text=True, timeout=300)
         if r.returncode == 0:
             out["dropin_class"] = json.loads(r.stdout.strip().splitlines()[-1])
         else:
             out["dropin_class"] = {"error": (r.stdout + r.stderr)[-300:]}
     return out
+
+
+def c2_rate(nbm, synth, dev, stream, flavor, steps=20):
+    """BASELINE config 2 (10M x 16 B, k = 7, one filter) device-resident, the same
+    timing as `value`: reported beside the C4 headline."""
+    import torch
+    wl = synth.C2
+    keys_np, _, kl = synth.keys_for(wl)
+    keys = torch.from_numpy(keys_np).to(dev)
+    words = torch.zeros(nbm.nwords(wl.m), dtype=torch.int64, device=dev)
+
+    def step():
+        with torch.cuda.stream(stream):
+            nbm.build_device(keys, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, flavor, words,
+                             stream=stream, overwrite=True)
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    ms = ev0.elapsed_time(ev1) / steps
+    B = algorithmic_bytes(wl.n, kl, wl.n * kl, wl.m, False)
+    return {"workload": wl.name, "value": round(wl.n * steps / el / 1e6, 3), "unit": "Mkeys/s",
+            "kernel_ms": round(ms, 5), "frac": round(B / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            "algorithmic_bytes_per_launch": B}
 
 
 def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=5):
@@ -196,18 +235,32 @@ def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=
     return res
 
 
-def latest_traffic(workload_name):
-    """Per-launch HBM bytes of the build kernel from the committed PMC summary
-    (profiles/*pmc*.json, written by tools/pmc_traffic.py), or None."""
+def latest_profile(workload_name, kind="pmc"):
+    """The committed profile summary of this workload for the current kernel
+    source: kind "pmc" = per-launch HBM bytes (profiles/*_pmc_*.json, written by
+    tools/pmc_traffic.py), "sq" = VALU counters (profiles/*_sq_*.json, written by
+    tools/sq_summary.py); None when none matches the kernel source hash."""
     best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json"))):
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", f"*_{kind}_*.json"))):
         try:
             d = json.load(open(f))
         except Exception:  # noqa: BLE001
             continue
         if d.get("workload") == workload_name and d.get("kernel_source_sha") == kernel_sha():
-            best = d
+            best = dict(d, source=d.get("source") or os.path.relpath(f, REPO))
     return best
+
+
+def valu_frac_of(sq):
+    """Build-weighted VALU fraction of the build kernels from an SQ summary:
+    sum of VALU floors (SQ_INSTS_VALU x 4 cycles / 1024 SIMDs / effective clock)
+    over the sum of the kernels' durations (tools/sq_summary.py)."""
+    if not sq:
+        return None
+    ks = [v for k, v in sq.get("kernels", {}).items() if k in sq.get("build_kernels", [])]
+    if not ks or any("valu_floor_us" not in v for v in ks):
+        return None
+    return round(sum(v["valu_floor_us"] for v in ks) / sum(v["avg_duration_us"] for v in ks), 4)
 
 
 def kernel_sha():
@@ -223,7 +276,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "merkle"],
+    ap.add_argument("--workload", default="c4", choices=["c1", "c2", "c3", "c4", "c5", "merkle"],
                     help="c1-c4: an independent filter per GPU (weak scaling); c5: one "
                          "cooperative filter over all GPUs (strong scaling, RCCL OR-merge); "
                          "merkle: the SSTable Merkle tree of C2's 10M x 16 B records per GPU")
@@ -232,6 +285,7 @@ def main():
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the host-buffer (H2D + build + D2H) rate measurement")
     ap.add_argument("--no-probe", action="store_true", help="skip the batch-probe rates")
+    ap.add_argument("--no-c2", action="store_true", help="skip the extra C2 line of the c4 run")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
 
@@ -308,13 +362,16 @@ def main():
     value = total_keys / elapsed / 1e6
     B = algorithmic_bytes(wl.n, key_len, total_key_bytes, wl.m, var_len)
     achieved = B / (kern_ms * 1e-3) / 1e9
-    pmc = latest_traffic(wl.name)
+    pmc = latest_profile(wl.name, "pmc")
+    sq = latest_profile(wl.name, "sq")
     roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 5),
                 "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
                 "kernel": "bloom_bin_kernel+bloom_tile_or_kernel (one build call)", "kernel_ms": round(kern_ms, 5),
                 "algorithmic_bytes_per_launch": B,
-                "traffic_source": (pmc or {}).get("source")}
+                "traffic_source": (pmc or {}).get("source"),
+                "valu_frac": valu_frac_of(sq),
+                "valu_source": (sq or {}).get("source")}
 
     out = {"metric": "bloom-filter build Mkeys/s (device-resident, k=7), 1/2/4/8 GPU",
            "value": round(value, 3), "unit": "Mkeys/s", "n_gpus": world, "steps": args.steps,
@@ -327,6 +384,8 @@ def main():
                       "flavor": ["libstdc++", "msvc-fnv1a"][args.flavor],
                       "parallelism": f"independent filter per GPU x{world}"},
            "roofline": roofline}
+    if rank == 0 and world == 1 and args.workload == "c4" and not args.no_c2:
+        out["c2"] = c2_rate(nbm, synth, dev, stream, args.flavor)
     if rank == 0 and world == 1 and not args.no_probe:
         out["probe"] = probe_rates(wl, keys, offs, key_len, seed, args.flavor, words, stream, dev)
     if rank == 0 and world == 1 and not args.no_host_path:

@@ -61,6 +61,9 @@ int nb_device_count(void);
 const char *nb_last_error(void);
 /* Release cached device scratch and streams on every device. */
 int nb_shutdown(void);
+/* Device builds enqueued by this process so far (every build entry point, any
+ * device): lets a caller check whether a path reached the GPU. */
+uint64_t nb_device_build_count(void);
 
 /* ------------------------------------------------- parameter formulas --- */
 /* BloomFilter::calculateSizeOfBitSet (BloomFilter.cpp:192-194), including the
@@ -93,6 +96,20 @@ int nb_build(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uin
 int nb_build_sharded(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                      uint32_t m, uint32_t k, uint64_t h2_seed, int flavor, uint64_t *words,
                      int nshards);
+
+/* The same build on the calling CPU thread: the drop-in class's path for small
+ * batches and for hosts without a usable GPU, e.g. the
+ * TypesManager deserialize -> add(one value) -> serialize round trip
+ * (System/TypesManager.cpp:74-92).  Same index arithmetic as the kernels
+ * (csrc/bloom_math.h); OR-accumulates into host `words`.  Reads key memory in
+ * whole aligned 8-byte words that hold key bytes, like the kernels: the buffer
+ * must stay addressable up to the aligned word holding its last byte. */
+int nb_build_cpu(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                 uint32_t m, uint32_t k, uint64_t h2_seed, int flavor, uint64_t *words);
+/* nb_probe on the calling CPU thread (same key-buffer rule as nb_build_cpu). */
+int nb_probe_cpu(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                 uint32_t m, uint32_t k, uint64_t h2_seed, int flavor, const uint64_t *words,
+                 uint8_t *out);
 
 /* Batch form of BloomFilter::possiblyContains (BloomFilter.cpp:67-80):
  * out[i] = 1 if all k bits of key i are set, else 0.  k == 0 answers 1

@@ -5,6 +5,9 @@
 //   nb_serialize       <- BloomFilter.cpp:88-129
 //   nb_deserialize     <- BloomFilter.cpp:131-190
 //   nb_std_hash        <- std::hash<std::string> (BloomFilter.cpp:59, merkle.cpp:27-28)
+//   nb_build_cpu       <- BloomFilter::add (BloomFilter.cpp:82-86) for a small batch on
+//                         the host: the drop-in class's small-batch / no-device path
+//                         (SURVEY §8(b)), with the kernels' own index arithmetic
 #include <cstdint>
 #include <cstring>
 #include <limits>
@@ -12,6 +15,8 @@
 
 #include "../../include/nasp_bloom.h"
 #include "bloom_math.h"
+
+int nb_internal_fail(int code, const char *msg);  // bloom_kernels.hip: the error slot
 
 extern "C" {
 
@@ -53,7 +58,8 @@ size_t nb_serialize(uint32_t m, uint32_t k, double p, uint32_t time_const, uint6
 
 int nb_deserialize(const uint8_t *img, size_t len, uint32_t *m, uint32_t *k, double *p,
                    uint32_t *time_const, uint64_t *h2_seed, uint64_t *words) {
-    if (!img || len < 28) return NB_ERR_ARG;
+    if (!img || len < 28)
+        return nb_internal_fail(NB_ERR_ARG, "serialized filter shorter than its 28-byte header");
     uint32_t mm;
     std::memcpy(&mm, img + 0, 4);
     if (m) *m = mm;
@@ -63,7 +69,8 @@ int nb_deserialize(const uint8_t *img, size_t len, uint32_t *m, uint32_t *k, dou
     if (h2_seed) std::memcpy(h2_seed, img + 20, 8);
     if (!words) return NB_OK;
     const size_t nbytes = (uint32_t)(mm + 7u) / 8u;
-    if (len < 28 + nbytes) return NB_ERR_ARG;
+    if (len < 28 + nbytes)
+        return nb_internal_fail(NB_ERR_ARG, "serialized filter shorter than its bit payload");
     const size_t nwords = ((size_t)mm + 63) / 64;
     if (nwords) words[nwords - 1] = 0;  // clear the partial last word before the copy
     if (nbytes) std::memcpy(words, img + 28, nbytes);
@@ -71,6 +78,92 @@ int nb_deserialize(const uint8_t *img, size_t len, uint32_t *m, uint32_t *k, dou
     if (mm & 63) words[nwords - 1] &= (1ull << (mm & 63)) - 1;
     return NB_OK;
 }
+
+}  // extern "C"
+
+namespace {
+// The kernels' word-stream hashes of key i on the host: aligned 8-byte words
+// that hold key bytes (never past the key's last aligned word), then the index
+// generator -- csrc/bloom_math.h, the code the kernels run.
+template <class F>
+void for_each_key_indices(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
+                          uint64_t n, const nb::FilterConsts &c, int flavor, F &&fn) {
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t b = offsets ? offsets[i] : i * (uint64_t)key_len;
+        const uint32_t len = (uint32_t)(offsets ? offsets[i + 1] - b : key_len);
+        const uintptr_t addr = reinterpret_cast<uintptr_t>(keys + b);
+        const uint32_t a = (uint32_t)(addr & 7);
+        const uint64_t *q = reinterpret_cast<const uint64_t *>(addr - a);
+        auto load = [q](uint32_t j) {
+            uint64_t w;
+            std::memcpy(&w, q + j, 8);
+            return w;
+        };
+        uint64_t h1, h2;
+        if (flavor == NB_FLAVOR_MSVC_FNV1A)
+            nb::hash_aligned_words<NB_FLAVOR_MSVC_FNV1A>(c, load, a, len, &h1, &h2);
+        else if (offsets)
+            nb::hash_aligned_words<NB_FLAVOR_LIBSTDCXX, decltype(load), false>(c, load, a, len, &h1, &h2);
+        else
+            nb::hash_aligned_words<NB_FLAVOR_LIBSTDCXX, decltype(load), true>(c, load, a, len, &h1, &h2);
+        nb::IndexGen g;
+        g.start(h1, h2, c);
+        fn(i, g);
+    }
+}
+
+int cpu_args(uint64_t n, uint32_t m, uint32_t k, int flavor, const void *keys, const void *words) {
+    if (flavor != NB_FLAVOR_LIBSTDCXX && flavor != NB_FLAVOR_MSVC_FNV1A)
+        return nb_internal_fail(NB_ERR_ARG, "unknown flavor");
+    if (n && k && m == 0) return nb_internal_fail(NB_ERR_ARG, "m == 0 with keys (reference divides by zero)");
+    if (n && k && (!keys || !words)) return nb_internal_fail(NB_ERR_ARG, "NULL keys or words");
+    return NB_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int nb_build_cpu(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                 uint32_t m, uint32_t k, uint64_t h2_seed, int flavor, uint64_t *words) {
+    const int rc = cpu_args(n, m, k, flavor, keys, words);
+    if (rc || n == 0 || k == 0) return rc;
+    nb::FilterConsts c = nb::make_consts(m, k, h2_seed, (uint32_t)flavor);
+    if (!offsets) nb::set_fixed_len(c, key_len);
+    for_each_key_indices(keys, offsets, key_len, n, c, flavor, [&](uint64_t, nb::IndexGen &g) {
+        for (uint32_t j = 0; j < k; ++j) {
+            if (j) g.next(c);
+            words[g.r >> 6] |= 1ull << (g.r & 63);
+        }
+    });
+    return NB_OK;
+}
+
+int nb_probe_cpu(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                 uint32_t m, uint32_t k, uint64_t h2_seed, int flavor, const uint64_t *words,
+                 uint8_t *out) {
+    if (n && !out) return nb_internal_fail(NB_ERR_ARG, "NULL out");
+    if (n && k == 0) {  // no hash closures: possiblyContains answers true
+        std::memset(out, 1, n);
+        return NB_OK;
+    }
+    const int rc = cpu_args(n, m, k, flavor, keys, words);
+    if (rc || n == 0) return rc;
+    nb::FilterConsts c = nb::make_consts(m, k, h2_seed, (uint32_t)flavor);
+    if (!offsets) nb::set_fixed_len(c, key_len);
+    for_each_key_indices(keys, offsets, key_len, n, c, flavor, [&](uint64_t i, nb::IndexGen &g) {
+        uint8_t hit = 1;
+        for (uint32_t j = 0; j < k && hit; ++j) {
+            if (j) g.next(c);
+            hit = (words[g.r >> 6] >> (g.r & 63)) & 1u;
+        }
+        out[i] = hit;
+    });
+    return NB_OK;
+}
+
+}  // extern "C"
+
+extern "C" {
 
 static size_t varint_len(uint64_t v) {
     size_t n = 1;

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1104,8 +1105,11 @@ int check_common(uint64_t n, uint32_t m, int flavor, const void *keys, const voi
 
 // Per-(device, stream) scratch of the tiled path: bucket cursors, spill flags and
 // the spill bitmap (all kept zero between builds by the tile kernel), and the
-// bucket array.
+// bucket array.  `mu` is held from the reservation through the last launch of a
+// build, so two host threads building on the same stream enqueue whole builds
+// (bin A, tile A, bin B, tile B), never interleaved kernels over one workspace.
 struct Workspace {
+    std::mutex mu;
     int dev = -1;
     hipStream_t st = nullptr;
     uint32_t *zeroed = nullptr;   // gcur [kShards*kMaxTiles] | spill_flag [kMaxTiles] |
@@ -1282,6 +1286,7 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     TileScratch sc;
     int rc;
     if ((rc = get_ws(st, &ws))) return rc;
+    std::lock_guard<std::mutex> lk(ws->mu);
     if ((rc = ws_reserve(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * sizeof(ENTRY), &sc)))
         return rc;
     size_t sort_bytes = kpb * c.k * 4;
@@ -1329,6 +1334,7 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
     TileScratch sc;
     int rc;
     if ((rc = get_ws(st, &ws))) return rc;
+    std::lock_guard<std::mutex> lk(ws->mu);
     const uint32_t rebin_x = (uint32_t)(((uint64_t)t1.cap * t1.G + kRebinSpan - 1) / kRebinSpan);
     // fine entries packed three per word (2^ts2 <= 2^21): capacity in words, the
     // entries' plus <= 2 pad slots per re-bin block of the shard
@@ -1491,6 +1497,8 @@ int launch_probe_f(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     return NB_OK;
 }
 
+std::atomic<uint64_t> g_device_builds{0};  // nb_device_build_count()
+
 int launch_build(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                  uint32_t m, uint32_t k, uint64_t seed, int flavor, uint64_t *words,
                  bool overwrite, hipStream_t st) {
@@ -1500,6 +1508,7 @@ int launch_build(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
     }
     FilterConsts c = nb::make_consts(m, k, seed, (uint32_t)flavor);
     if (!offsets) nb::set_fixed_len(c, key_len);
+    g_device_builds.fetch_add(1, std::memory_order_relaxed);
     return flavor == NB_FLAVOR_MSVC_FNV1A
                ? launch_build_f<NB_FLAVOR_MSVC_FNV1A>(keys, offsets, key_len, n, c, words,
                                                       overwrite, st)
@@ -1553,9 +1562,12 @@ int open_device(int device, DevScratch **out) {
         return fail(NB_ERR_ARG, "device index out of range");
     NB_HIP(hipSetDevice(device));
     DevScratch &d = g_dev[device];
-    if (!d.init) {
-        NB_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-        d.init = true;
+    {
+        std::lock_guard<std::mutex> lk(d.mu);  // the first callers on a device race here
+        if (!d.init) {
+            NB_HIP(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+            d.init = true;
+        }
     }
     *out = &d;
     return NB_OK;
@@ -1606,6 +1618,8 @@ int nb_device_count(void) {
 }
 
 const char *nb_last_error(void) { return g_last_error.c_str(); }
+
+uint64_t nb_device_build_count(void) { return g_device_builds.load(std::memory_order_relaxed); }
 
 int nb_shutdown(void) {
     {

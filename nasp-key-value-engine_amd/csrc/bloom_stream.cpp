@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -217,6 +218,7 @@ int nb_builder_create(uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
 
 int nb_builder_add(nb_builder *b, const uint8_t *key, uint64_t len) {
     if (!b || (len && !key)) return nb_internal_fail(NB_ERR_ARG, "NULL builder or key");
+    if (b->m == 0 && b->k) return nb_internal_fail(NB_ERR_ARG, "add() on a filter with m == 0");
     if (len > kChunkBytes) {  // one oversized key: its own chunk, synchronously
         int rc = b->submit();
         if (rc) return rc;
@@ -258,6 +260,14 @@ int nb_builder_add_batch(nb_builder *b, const uint8_t *keys, const uint64_t *off
     SB_HIP(hipSetDevice(b->ss->dev));
     int rc = b->submit();  // the partly packed chunk first
     if (rc) return rc;
+    if (!offsets && key_len > kChunkBytes) {
+        // fixed-length keys longer than a chunk: each one through the oversized-key
+        // path (its own device buffer), as variable-length keys of that size go
+        for (uint64_t i = 0; i < n; ++i)
+            if ((rc = nb_builder_add(b, keys + i * (uint64_t)key_len, key_len))) return rc;
+        b->slot(b->cur).h_offs[0] = 0;
+        return NB_OK;
+    }
     SlotSet *ss = b->ss;
     uint64_t i = 0;
     while (i < n) {
@@ -347,17 +357,45 @@ int drain(nb_builder *b) {
     return NB_OK;
 }
 
+// Download device words [0, nwords) into host `dst` through the slot set's pinned
+// key chunks (two at a time: chunk i+1's DMA overlaps chunk i's host copy), so the
+// concurrent per-owner downloads of the merge are plain DMA into memory the
+// library owns -- none of them relies on the runtime's staging of pageable copies.
+int download_pinned(SlotSet *ss, const uint64_t *d, uint64_t nwords, uint64_t *dst) {
+    const uint64_t per = kChunkBytes / 8;  // words per chunk
+    const uint64_t pieces = (nwords + per - 1) / per;
+    for (uint64_t i = 0; i < pieces + 1; ++i) {
+        if (i < pieces) {
+            Slot &sl = ss->s[i % 2];
+            const uint64_t w = std::min(per, nwords - i * per);
+            SB_HIP(hipMemcpyAsync(sl.h_keys, d + i * per, w * 8, hipMemcpyDeviceToHost, ss->comp));
+            SB_HIP(hipEventRecord(sl.built, ss->comp));
+        }
+        if (i > 0) {
+            Slot &sl = ss->s[(i - 1) % 2];
+            SB_HIP(hipEventSynchronize(sl.built));
+            const uint64_t w = std::min(per, nwords - (i - 1) * per);
+            std::memcpy(dst + (i - 1) * per, sl.h_keys, w * 8);
+        }
+    }
+    return NB_OK;
+}
+
 // Owner o's step of the merge: OR word slice [lo, lo + len) of every other
 // partial into its own, reading the sources in place (same device, or a peer over
 // xGMI with peer access enabled) in one stream-ordered kernel, then download the
 // merged slice into the caller's words.  A source the owner cannot address
-// directly is first brought over with a blocking hipMemcpyPeer.
+// directly is first brought over with a blocking hipMemcpyPeer (complete on
+// return, before the OR kernel is enqueued); NB_SHARDED_STAGE=1 forces that
+// staging branch for every source, so a one-GPU box can test it.
 int merge_slice(std::vector<nb_builder *> &bs, int o, uint64_t lo, uint64_t len, uint64_t *words,
                 const std::vector<char> &peer, int ndev) {
     nb_builder *own = bs[o];
     const int dev = own->ss->dev;
     hipStream_t st = own->ss->comp;
     SB_HIP(hipSetDevice(dev));
+    const char *force = std::getenv("NB_SHARDED_STAGE");
+    const bool stage_all = force && *force && *force != '0';
     std::vector<const uint64_t *> srcs;
     uint64_t *tmp = nullptr;
     size_t staged = 0;
@@ -365,7 +403,7 @@ int merge_slice(std::vector<nb_builder *> &bs, int o, uint64_t lo, uint64_t len,
     for (size_t s = 0; s < bs.size() && !rc; ++s) {
         if ((int)s == o) continue;
         const int sdev = bs[s]->ss->dev;
-        if (sdev == dev || peer[(size_t)dev * ndev + sdev]) {
+        if (!stage_all && (sdev == dev || peer[(size_t)dev * ndev + sdev])) {
             srcs.push_back(bs[s]->ss->d_words + lo);
             continue;
         }
@@ -381,12 +419,10 @@ int merge_slice(std::vector<nb_builder *> &bs, int o, uint64_t lo, uint64_t len,
             srcs.push_back(tmp + (staged++) * len);
     }
     if (!rc) rc = nb_internal_or_gather(own->ss->d_words + lo, srcs.data(), (uint32_t)srcs.size(), len, st);
-    hipError_t e1 = hipSuccess;
-    if (!rc) e1 = hipMemcpyAsync(words + lo, own->ss->d_words + lo, len * 8, hipMemcpyDeviceToHost, st);
-    const hipError_t e2 = hipStreamSynchronize(st);
+    if (!rc) rc = download_pinned(own->ss, own->ss->d_words + lo, len, words + lo);
+    const hipError_t e2 = hipStreamSynchronize(st);  // tmp is read by the OR kernel
     if (tmp) (void)hipFree(tmp);
     if (rc) return rc;
-    SB_HIP(e1);
     SB_HIP(e2);
     return NB_OK;
 }

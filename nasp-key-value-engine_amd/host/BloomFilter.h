@@ -6,22 +6,26 @@
 // filter writers and readers (SSTableRaw.cpp:539,620; SSTableComp.cpp:476,555),
 // TypesManager (System/TypesManager.cpp:58-107).
 //
-// What changes inside:
+// What changes inside (SURVEY.md §8(b) batching strategy):
 //   - the bit set is a std::vector<uint64_t> (little-endian words == the
 //     serialized LSB-first byte image) instead of vector<bool>;
-//   - add() packs the key into a streaming builder (nb_builder_*, include/
-//     nasp_bloom.h): pinned host chunks whose upload and device build overlap the
-//     packing of the next keys; the filter is downloaded when it is next read
-//     (possiblyContains / serialize / copy), which also returns the builder's
-//     buffers to the library's pool;
+//   - add() appends the key to a packed host batch (16 MB chunks: bytes, and
+//     offsets only once the chunk's key lengths differ); the batch is built when
+//     the filter is next read (possiblyContains / serialize / copy);
+//   - a batch of at least hostBatchLimit() keys (default 4 096, the same cut-over
+//     the library's `auto` path uses) is built on the GPU through the streaming
+//     builder (nb_builder_*), chunk by chunk; a smaller one -- e.g. the
+//     TypesManager deserialize -> add(one value) -> serialize round trip
+//     (TypesManager.cpp:74-92) -- is built on the host by nb_build_cpu with the
+//     kernels' own index arithmetic (csrc/bloom_math.h): no device round trip;
+//   - if the device build fails (no GPU, device error) the batch is built on the
+//     host instead and one line goes to std::cerr, in the reference's error style
+//     (SSTableComp.cpp:543): add() and serialize() never throw for it;
 //   - possiblyContains() of one key is evaluated on the host against the same
-//     bits (the latency-bound lookup path, SSTManager.cpp:203,224), with the
-//     exact same index arithmetic the kernels use (csrc/bloom_math.h).
+//     bits (the latency-bound lookup path, SSTManager.cpp:203,224).
 // Semantics kept: default-constructed filter answers true for every key
 // (BloomFilter.cpp:26,67-80); add() after deserialize() ORs into the loaded bits
 // (TypesManager.cpp:84-86); serialize() is byte-identical (BloomFilter.cpp:88-129).
-//
-// A failed device build throws std::runtime_error: there is no CPU fallback.
 #pragma once
 
 // The reference header's includes are kept: its callers rely on them
@@ -50,13 +54,21 @@ private:
 
     int flavor;                 // std::hash flavour (NB_FLAVOR_*)
     int device = 0;
-    // keys added since the last read, in flight on the device (mutable: const
-    // readers materialise them); bits_zero: `bits` is still all zero
-    mutable struct nb_builder *builder = nullptr;
-    mutable bool bits_zero = true;
+    // Keys added since the last read, packed (mutable: const readers build them).
+    struct Chunk {
+        std::vector<uint8_t> bytes;
+        std::vector<uint64_t> offs;  // n + 1 entries once lengths differ (fixed < 0)
+        int64_t fixed = -1;          // common key length (-1: no key yet, -2: mixed)
+        uint64_t n = 0;
+    };
+    mutable std::vector<Chunk> pending;
+    mutable uint64_t pending_n = 0;
+    mutable bool bits_zero = true;   // `bits` is still all zero
+    mutable bool last_on_device = false;
 
     void flush() const;
-    void release() noexcept;
+    bool build_on_device() const;
+    void build_on_host() const;
 
 public:
     // Constructor
@@ -66,9 +78,9 @@ public:
     // the built filter): a copy materialises the source's pending keys first.
     BloomFilter(const BloomFilter &o);
     BloomFilter &operator=(const BloomFilter &o);
-    BloomFilter(BloomFilter &&o) noexcept;
-    BloomFilter &operator=(BloomFilter &&o) noexcept;
-    ~BloomFilter();
+    BloomFilter(BloomFilter &&o) noexcept = default;
+    BloomFilter &operator=(BloomFilter &&o) noexcept = default;
+    ~BloomFilter() = default;
 
     // Add an element to the Bloom Filter
     void add(const std::string& elem);
@@ -91,12 +103,17 @@ public:
     // a Linux build of the reference) or NB_FLAVOR_MSVC_FNV1A (files written by
     // the authors' Windows build, e.g. the reference's committed *.sst filters).
     static void setDefaultFlavor(int flavor);
+    // Batches of fewer keys than this are built on the host (default 4 096).
+    static void setHostBatchLimit(uint64_t keys);
+    static uint64_t hostBatchLimit();
     void setFlavor(int f) { flush(); flavor = f; }
     void setDevice(int d) { device = d; }
     // Add many keys at once (same result as add() on each).
     void addBatch(const std::vector<std::string>& elems);
     // Build every pending key now (no-op if none).
     void materialize() const { flush(); }
+    // Whether the last materialised batch was built on the GPU.
+    bool lastBuildOnDevice() const { return last_on_device; }
     unsigned int bitCount() const { return m; }
     unsigned int hashCount() const { return k; }
 };

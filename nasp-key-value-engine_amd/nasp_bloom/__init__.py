@@ -17,5 +17,5 @@ is the Python binding used by tests/ and bench.py:
 from ._lib import (FLAVOR_LIBSTDCXX, FLAVOR_MSVC_FNV1A, NaspBloomError, lib)  # noqa: F401
 from .api import (BloomFilter, Builder, MerkleTree, build_device, merkle_device, merkle_host,  # noqa: F401
                   merkle_tree_size, std_hash, build_host, build_host_sharded, deserialize, nwords, or_merge_device,  # noqa: F401
-                  probe_device, probe_host, seed_from_time, serialize, size_of_bitset,
+                  probe_device, probe_host, build_cpu, probe_cpu, device_build_count, seed_from_time, serialize, size_of_bitset,
                   num_hashes)

@@ -29,6 +29,7 @@ _SIGS = {
     "nb_device_count": (C.c_int, []),
     "nb_last_error": (C.c_char_p, []),
     "nb_shutdown": (C.c_int, []),
+    "nb_device_build_count": (C.c_uint64, []),
     "nb_size_of_bitset": (C.c_uint32, [C.c_uint32, C.c_double]),
     "nb_num_hashes": (C.c_uint32, [C.c_uint32, C.c_uint32]),
     "nb_seed_from_time": (C.c_uint64, [C.c_uint32]),
@@ -37,6 +38,10 @@ _SIGS = {
                            C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_int]),
     "nb_build_sharded": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
                                    C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_int]),
+    "nb_build_cpu": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
+                               C.c_uint32, C.c_uint64, C.c_int, C.c_void_p]),
+    "nb_probe_cpu": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
+                               C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p]),
     "nb_probe": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,
                            C.c_uint32, C.c_uint64, C.c_int, C.c_void_p, C.c_void_p, C.c_int]),
     "nb_build_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_uint32,

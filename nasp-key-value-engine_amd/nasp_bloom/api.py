@@ -114,6 +114,32 @@ def build_host(keys: np.ndarray, offsets: np.ndarray | None, key_len: int, n: in
     check(rc, "nb_build")
 
 
+def build_cpu(keys: np.ndarray, offsets: np.ndarray | None, key_len: int, n: int, m: int, k: int,
+              seed: int, flavor: int, words: np.ndarray) -> None:
+    """nb_build_cpu: the same build on the calling CPU thread (the drop-in classes'
+    small-batch / no-device path); keys need the aligned-word slack
+    the packers here add."""
+    assert words.dtype == np.uint64 and words.flags.c_contiguous
+    rc = lib().nb_build_cpu(_np_ptr(keys), _np_ptr(offsets), key_len, n, m, k, seed, flavor,
+                            _np_ptr(words))
+    check(rc, "nb_build_cpu")
+
+
+def probe_cpu(keys: np.ndarray, offsets: np.ndarray | None, key_len: int, n: int, m: int, k: int,
+              seed: int, flavor: int, words: np.ndarray) -> np.ndarray:
+    """nb_probe_cpu: possiblyContains for a (small) batch on the calling CPU thread."""
+    out = np.zeros(max(n, 1), dtype=np.uint8)
+    rc = lib().nb_probe_cpu(_np_ptr(keys), _np_ptr(offsets), key_len, n, m, k, seed, flavor,
+                            _np_ptr(words), _np_ptr(out))
+    check(rc, "nb_probe_cpu")
+    return out[:n]
+
+
+def device_build_count() -> int:
+    """Device builds this process has enqueued (nb_device_build_count)."""
+    return int(lib().nb_device_build_count())
+
+
 def build_host_sharded(keys: np.ndarray, offsets: np.ndarray | None, key_len: int, n: int, m: int,
                        k: int, seed: int, flavor: int, words: np.ndarray, nshards: int = 0) -> None:
     """nb_build over `nshards` key ranges (0: one per visible device), shard s on
@@ -212,12 +238,14 @@ def _pack(keys: list[bytes]):
 class BloomFilter:
     """Mirror of the reference `BloomFilter` (BloomFilter/BloomFilter.h:12-42)."""
 
-    BATCH_LIMIT = 1 << 20  # pending keys before an automatic device build
+    BATCH_LIMIT = 1 << 20  # pending keys before an automatic build
+    HOST_BATCH_LIMIT = 4096  # smaller batches are built on the host (nb_build_cpu)
 
     def __init__(self, n: int | None = None, falsePositiveRate: float | None = None, *,
                  flavor: int = FLAVOR_LIBSTDCXX, device: int = 0, time_const: int | None = None):
         self.flavor = flavor
         self.device = device
+        self.last_on_device = False
         self._pending: list[bytes] = []
         if n is None:  # BloomFilter() -- BloomFilter.cpp:26: no closures, no bits
             self.m, self.k, self.p, self.timeConst, self.h2_seed = 0, 0, 0.0, 0, 0
@@ -247,8 +275,18 @@ class BloomFilter:
         if self.k == 0:
             return  # no closures: add() sets nothing (BloomFilter.cpp:82-86)
         buf, offs = _pack(keys)
-        build_host(buf, offs, 0, len(keys), self.m, self.k, self.h2_seed, self.flavor,
-                   self.words, self.device)
+        self.last_on_device = False
+        if len(keys) >= self.HOST_BATCH_LIMIT:
+            try:
+                build_host(buf, offs, 0, len(keys), self.m, self.k, self.h2_seed, self.flavor,
+                           self.words, self.device)
+                self.last_on_device = True
+                return
+            except NaspBloomError as e:  # the reference's error style: report, carry on
+                import sys
+                print(f"[BloomFilter] GPU build failed ({e}); building {len(keys)} keys on the host",
+                      file=sys.stderr)
+        build_cpu(buf, offs, 0, len(keys), self.m, self.k, self.h2_seed, self.flavor, self.words)
 
     def add(self, elem: bytes | str) -> None:
         self._pending.append(elem.encode() if isinstance(elem, str) else bytes(elem))
@@ -270,6 +308,9 @@ class BloomFilter:
         if self.k == 0:
             return np.ones(len(keys), dtype=np.uint8)
         buf, offs = _pack(keys)
+        if len(keys) < self.HOST_BATCH_LIMIT:  # single-key lookups stay on the host
+            return probe_cpu(buf, offs, 0, len(keys), self.m, self.k, self.h2_seed, self.flavor,
+                             self.words)
         return probe_host(buf, offs, 0, len(keys), self.m, self.k, self.h2_seed, self.flavor,
                           self.words, self.device)
 

@@ -1,13 +1,18 @@
 // Drop-in class test: drives nasp-key-value-engine_amd/host/BloomFilter the way
 // the reference's callers do and checks every image bit for bit against the
-// oracle (oracle/bloom_oracle.c).  Needs a GPU (the class builds on the device).
+// oracle (oracle/bloom_oracle.c).  Runs with or without a GPU: batches of at
+// least BloomFilter::hostBatchLimit() keys are built on the device when one is
+// visible (checked), smaller ones -- and every batch on a GPU-less host, after
+// one std::cerr line per failed device build -- on the host.
 //   1. reference test program flow (BloomFilter/main.cpp:28-117): BF(20, 0.05),
 //      10 names added, membership of added / absent names, BF(10, 0.1) round trip;
 //   2. SSTable::build usage (SSTable/SSTable.cpp:28-35): BF(records.size(), 0.01),
 //      add() per record key, copy-assign into a member, serialize();
 //   3. TypesManager usage (System/TypesManager.cpp:74-107): deserialize, add,
 //      serialize (accumulate), then probe;
-//   4. the reference's committed MSVC filters with the FNV flavour.
+//   4. the reference's committed MSVC filters with the FNV flavour;
+//   5. device / host placement: a large batch reaches the GPU (when there is
+//      one), a TypesManager round trip launches no device build.
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -60,10 +65,8 @@ static void header(const std::vector<uint8_t> &img, uint32_t *m, uint32_t *k, do
 }
 
 int main() {
-    if (nb_device_count() < 1) {
-        std::printf("SKIP: no GPU\n");
-        return 77;
-    }
+    const bool gpu = nb_device_count() > 0;
+    std::printf("devices: %d\n", nb_device_count());
     // 1. reference test program flow
     {
         BloomFilter bf(20, 0.05);
@@ -111,12 +114,14 @@ int main() {
         uint32_t m, k, tc; double p; uint64_t seed;
         header(img, &m, &k, &p, &tc, &seed);
         EXPECT(img == oracle_image(recs, m, k, p, tc, seed, 0), "SSTable-style build image");
+        EXPECT(member.lastBuildOnDevice() == gpu, "50k-key batch built on the GPU iff one is visible");
         int present = 0;
         for (auto &r : recs) present += member.possiblyContains(r);
         EXPECT(present == (int)recs.size(), "no false negatives");
     }
     // 3. TypesManager usage: deserialize -> add -> serialize accumulates
     {
+        const uint64_t launches = nb_device_build_count();
         BloomFilter bf(1000, 0.01);
         bf.add("alpha");
         auto first = bf.serialize();
@@ -129,6 +134,8 @@ int main() {
         EXPECT(img == oracle_image({"alpha", "beta", std::string("\0gamma", 6)}, m, k, p, tc, seed, 0),
                "accumulate after deserialize");
         EXPECT(again.possiblyContains("alpha") && again.possiblyContains("beta"), "accumulated keys");
+        EXPECT(!again.lastBuildOnDevice() && nb_device_build_count() == launches,
+               "TypesManager round trip stays on the host (no device build)");
         BloomFilter def;
         EXPECT(def.possiblyContains("anything"), "default filter answers true");
     }
@@ -149,6 +156,32 @@ int main() {
                "re-adding the members leaves the MSVC image unchanged");
         BloomFilter::setDefaultFlavor(NB_FLAVOR_LIBSTDCXX);
     }
+    // 5. the host/device cut-over at hostBatchLimit() keys, both flavours, mixed
+    //    key lengths (offsets chunk) and one length (fixed chunk), empty keys
+    for (int flavor = 0; flavor < 2; ++flavor) {
+        BloomFilter::setDefaultFlavor(flavor);
+        for (uint64_t n : {BloomFilter::hostBatchLimit() - 1, BloomFilter::hostBatchLimit()}) {
+            for (int mixed = 0; mixed < 2; ++mixed) {
+                std::vector<std::string> keys;
+                for (uint64_t i = 0; i < n; ++i) {
+                    char b[48];
+                    const int l = std::snprintf(b, sizeof b, "k%015llu", (unsigned long long)i * 7919);
+                    keys.emplace_back(b, mixed ? (size_t)(i % 23) : (size_t)l);
+                }
+                BloomFilter bf((unsigned)n, 0.01);
+                const uint64_t before = nb_device_build_count();
+                for (auto &x : keys) bf.add(x);
+                auto img = bytes_of(bf.serialize());
+                uint32_t m, k, tc; double p; uint64_t seed;
+                header(img, &m, &k, &p, &tc, &seed);
+                EXPECT(img == oracle_image(keys, m, k, p, tc, seed, flavor), "cut-over image");
+                const bool dev = n >= BloomFilter::hostBatchLimit() && gpu;
+                EXPECT(bf.lastBuildOnDevice() == dev, "batch placement");
+                EXPECT((nb_device_build_count() > before) == dev, "device builds only for large batches");
+            }
+        }
+    }
+    BloomFilter::setDefaultFlavor(NB_FLAVOR_LIBSTDCXX);
     nb_shutdown();
     std::printf(failures ? "FAILED %d\n" : "drop-in OK\n", failures);
     return failures ? 1 : 0;

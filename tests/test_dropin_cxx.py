@@ -1,6 +1,8 @@
-"""The C++ drop-in class (host/BloomFilter.h): it compiles and links against the
-C ABI library on CPU; on the GPU box tests/cpp/test_dropin.cpp runs the
-reference callers' usage patterns and checks every image against the oracle."""
+"""The C++ drop-in class (host/BloomFilter.h): tests/cpp/test_dropin.cpp runs the
+reference callers' usage patterns and checks every image against the oracle --
+on the CPU box with no device visible (every batch then built on the host, large
+ones after a std::cerr line: SURVEY §8(b)'s fallback), and on the GPU box, where
+large batches must reach the device and small ones must not."""
 import os
 import subprocess
 
@@ -26,11 +28,22 @@ def test_dropin_compiles_and_links(tmp_path, built):
     assert build_dropin(tmp_path).exists()
 
 
+def test_dropin_without_gpu(tmp_path, built):
+    """HIP_VISIBLE_DEVICES= (empty): no device; the class still produces the
+    reference bytes, and says on stderr that it built on the host."""
+    exe = build_dropin(tmp_path)
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="")
+    out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "devices: 0" in out.stdout and "drop-in OK" in out.stdout
+    assert "[BloomFilter] GPU build failed" in out.stderr
+
+
 @pytest.mark.gpu
 def test_dropin_on_gpu(tmp_path, built):
     exe = build_dropin(tmp_path)
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600)
-    if out.returncode == 77:
-        pytest.skip("no GPU")
     assert out.returncode == 0, out.stdout + out.stderr
+    assert "devices: 0" not in out.stdout, "the GPU test ran without a device"
     assert "drop-in OK" in out.stdout
+    assert "GPU build failed" not in out.stderr

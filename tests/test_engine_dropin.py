@@ -109,6 +109,36 @@ def test_reference_engine_framing(tmp_path, oracle, mode, bs, built):
     assert (m, k) == (9586, 7)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["raw", "comp"])
+@pytest.mark.parametrize("bs", [4096, 75])
+def test_frame_filter_device_matches_reference_file(tmp_path, oracle, mode, bs, built):
+    """nb_frame_filter_device (filter words still in HBM, payload copied D2H
+    straight into its place in the framed region) writes the
+    reference engine's filter file byte for byte, and equals nb_frame_filter."""
+    if not os.path.exists(REF_ENGINE):
+        pytest.skip("oracle/_ref/ref_engine not built (needs /root/reference)")
+    import torch
+    import nasp_bloom as nbm
+    run_engine(REF_ENGINE, tmp_path, mode, 1000, bs)
+    (path,) = filter_files(tmp_path)
+    raw = open(path, "rb").read()
+    comp = mode == "comp"
+    m, k, p, tc, seed, words = nbm.deserialize(parse_framed(raw, comp))
+    h = nbm.lib()
+    dw = torch.from_numpy(words.view(np.int64)).to("cuda:0")
+    torch.cuda.synchronize()
+    size = h.nb_framed_filter_size(m, 1 if comp else 0, bs)
+    dev_out = np.full(size, 0xEE, np.uint8)
+    rc = h.nb_frame_filter_device(m, k, p, tc, seed, dw.data_ptr(), 1 if comp else 0, bs,
+                                  dev_out.ctypes.data, None)
+    assert rc == 0, h.nb_last_error()
+    host_out = np.zeros(size, np.uint8)
+    assert h.nb_frame_filter(m, k, p, tc, seed, words.ctypes.data, 1 if comp else 0, bs,
+                             host_out.ctypes.data) == size
+    assert dev_out.tobytes() == host_out.tobytes() == raw
+
+
 @pytest.mark.parametrize("mode", ["raw", "comp"])
 def test_reference_engine_tiered_compaction(tmp_path, oracle, mode, built):
     """The reference engine's size-tiered compaction output filter (k-way merged,

@@ -150,3 +150,35 @@ def test_builder_k0_and_errors(dev):
             b.finish()
     with pytest.raises(nbm.NaspBloomError):
         nbm.Builder(100, 3, SEED, flavor=7)
+
+
+def test_nb_build_fixed_key_longer_than_a_chunk(dev, oracle):
+    """Fixed-length keys longer than the builder's 16 MiB chunk (nb_build ->
+    add_batch) take the oversized-key path instead of overrunning the chunk."""
+    import nasp_bloom as nbm
+    kl = (16 << 20) + 1000
+    n = 2
+    buf = np.random.default_rng(5).integers(0, 256, n * kl + 16, dtype=np.uint8)
+    m, k = 4099, 5
+    w = np.zeros(nbm.nwords(m), np.uint64)
+    nbm.build_host(buf, None, kl, n, m, k, SEED, 0, w)
+    np.testing.assert_array_equal(w, oracle.build(0, buf, None, kl, n, m, k, SEED))
+
+
+def test_python_mirror_places_batches(dev, oracle):
+    """The Python BloomFilter mirror: a batch of >= HOST_BATCH_LIMIT keys is built
+    on the device (a device build is counted), a smaller one on the host; both
+    bit-exact with the oracle."""
+    import nasp_bloom as nbm
+    from golden_util import pack
+    for n, on_dev in ((nbm.BloomFilter.HOST_BATCH_LIMIT - 1, False),
+                      (nbm.BloomFilter.HOST_BATCH_LIMIT, True)):
+        keys = [b"user%012d" % i for i in range(n)]
+        bf = nbm.BloomFilter(n, 0.01, time_const=1748963255)
+        before = nbm.device_build_count()
+        bf.add_batch(keys)
+        img = bf.serialize()
+        assert bf.last_on_device == on_dev and (nbm.device_build_count() > before) == on_dev
+        buf, offs = pack(keys)
+        want = oracle.build(0, buf, offs, 0, n, bf.m, bf.k, bf.h2_seed)
+        assert img == nbm.serialize(bf.m, bf.k, bf.p, bf.timeConst, bf.h2_seed, want)

@@ -95,6 +95,34 @@ def test_concurrent_device_builds_on_streams(nbm, oracle):
                                       oracle.build(0, ks, None, 16, n, m, k, SEED))
 
 
+def test_two_threads_one_stream(nbm, oracle):
+    """Two host threads building different filters on the SAME stream: the
+    per-(device, stream) workspace is held for a whole build, so the kernels of
+    the two builds never interleave over one set of buckets and cursors."""
+    import torch
+    from nasp_bloom import synth
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(device=dev)
+    n, m, k = 300_000, 2_875_519, 7
+    keysets = [synth.fixed_keys(n, 16, seed=synth.SEED + 200 + t) for t in range(2)]
+    with torch.cuda.stream(st):
+        kts = [torch.from_numpy(ks).to(dev) for ks in keysets]
+    st.synchronize()
+    words = [torch.zeros(nbm.nwords(m), dtype=torch.int64, device=dev) for _ in keysets]
+
+    def job(i):
+        def f():
+            for _ in range(20):
+                nbm.build_device(kts[i], None, 16, n, m, k, SEED, 0, words[i], stream=st,
+                                 overwrite=True)
+        return f
+    _run_threads([job(i) for i in range(2)])
+    st.synchronize()
+    for i, ks in enumerate(keysets):
+        np.testing.assert_array_equal(words[i].cpu().numpy().view(np.uint64),
+                                      oracle.build(0, ks, None, 16, n, m, k, SEED))
+
+
 def test_errors_stay_in_their_thread(nbm):
     """nb_last_error is per thread: a failing call does not change another
     thread's successful call's message state."""

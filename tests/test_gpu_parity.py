@@ -191,6 +191,16 @@ def test_varlen_c3_shape(dev, oracle, flavor, shift, build_path):
     np.testing.assert_array_equal(got, want)
 
 
+def test_fnv_c2_full_size(dev, oracle):
+    """The MSVC FNV-1a flavour at C2's full size (10M x 16 B, k = 7), bit-exact."""
+    from nasp_bloom import synth
+    w = synth.C2
+    buf, offs, kl = synth.keys_for(w)
+    got = dev_build(dev, buf, offs, kl, w.n, w.m, w.k, SEED, flavor=1)
+    np.testing.assert_array_equal(got, oracle_build_threaded(oracle, 1, buf, offs, kl, w.n, w.m,
+                                                             w.k, SEED))
+
+
 @pytest.mark.parametrize("key_len,shift", [(16, 4), (32, 0), (7, 1), (1, 0), (64, 5), (100, 0)])
 def test_fixed_stride_layouts(dev, oracle, key_len, shift, build_path):
     from nasp_bloom import synth
@@ -515,6 +525,25 @@ def test_c3_full_size_properties(dev, oracle):
     assert 0.45 < fill < 0.55
     # and bit-exact at full size: the oracle over all 100M keys, 16 threads
     np.testing.assert_array_equal(fh, oracle_build_threaded(oracle, 0, buf, offs, 0, w.n, w.m,
+                                                            w.k, SEED))
+
+
+def test_fnv_c3_full_size(dev, oracle):
+    """The MSVC FNV-1a flavour at C3's full size (100M var-length 8-64 B keys),
+    bit-exact against the oracle run over 16 key ranges."""
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    w = synth.C3
+    buf, offs = synth.var_keys(w.n)
+    kt = t_u8(buf, dev)
+    ot = t_u64(offs, dev)
+    full = torch.zeros(nbm.nwords(w.m), dtype=torch.int64, device=dev)
+    nbm.build_device(kt, ot, 0, w.n, w.m, w.k, SEED, 1, full)
+    torch.cuda.synchronize()
+    del kt, ot
+    fh = full.cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(fh, oracle_build_threaded(oracle, 1, buf, offs, 0, w.n, w.m,
                                                             w.k, SEED))
 
 

@@ -70,3 +70,22 @@ def test_sharded_accumulates_and_edges(nbm, oracle):
         nbm.build_host_sharded(buf, offs, 0, 10, 0, 3, SEED, 0, np.zeros(1, np.uint64), 2)
     with pytest.raises(nbm.NaspBloomError):
         nbm.build_host_sharded(buf, offs, 0, 10, m, 3, SEED, 7, words, 2)
+
+
+@pytest.mark.parametrize("nshards", [2, 3, 8])
+def test_sharded_forced_staging(nbm, oracle, monkeypatch, nshards):
+    """NB_SHARDED_STAGE=1: every source of the slice merge goes through the
+    blocking hipMemcpyPeer staging branch (taken for real only between devices
+    without peer access), bit-exact against the oracle, both key layouts."""
+    from nasp_bloom import synth
+    monkeypatch.setenv("NB_SHARDED_STAGE", "1")
+    n = 300_007
+    buf, offs = synth.var_keys(n)
+    m, k = 2_875_519, 7
+    words = np.zeros(nbm.nwords(m), np.uint64)
+    nbm.build_host_sharded(buf, offs, 0, n, m, k, SEED, 0, words, nshards)
+    np.testing.assert_array_equal(words, oracle.build(0, buf, offs, 0, n, m, k, SEED))
+    fb = synth.fixed_keys(n, 16)
+    fw = np.zeros(nbm.nwords(m), np.uint64)
+    nbm.build_host_sharded(fb, None, 16, n, m, k, SEED, 1, fw, nshards)
+    np.testing.assert_array_equal(fw, oracle.build(1, fb, None, 16, n, m, k, SEED))
