@@ -1167,7 +1167,10 @@ int ws_reserve(Workspace &w, uint32_t m, size_t bucket_bytes, TileScratch *sc,
         w.zeroed = nullptr;
         w.zeroed_bytes = 0;
         NB_HIP(hipMalloc(&w.zeroed, zb));
-        NB_HIP(hipMemset(w.zeroed, 0, zb));
+        // on the workspace's stream: a blocking hipMemset runs on the null stream,
+        // which non-blocking streams do not wait for (same hazard as the sharded
+        // merge's staging copy)
+        NB_HIP(hipMemsetAsync(w.zeroed, 0, zb, w.st));
         w.zeroed_bytes = zb;
     }
     int rc;

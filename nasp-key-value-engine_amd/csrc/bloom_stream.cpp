@@ -385,9 +385,9 @@ int download_pinned(SlotSet *ss, const uint64_t *d, uint64_t nwords, uint64_t *d
 // partial into its own, reading the sources in place (same device, or a peer over
 // xGMI with peer access enabled) in one stream-ordered kernel, then download the
 // merged slice into the caller's words.  A source the owner cannot address
-// directly is first brought over with a blocking hipMemcpyPeer (complete on
-// return, before the OR kernel is enqueued); NB_SHARDED_STAGE=1 forces that
-// staging branch for every source, so a one-GPU box can test it.
+// directly is first brought over with a peer copy on the owner's stream (ordered
+// before the OR kernel); NB_SHARDED_STAGE=1 forces that staging branch for every
+// source, so a one-GPU box can test it.
 int merge_slice(std::vector<nb_builder *> &bs, int o, uint64_t lo, uint64_t len, uint64_t *words,
                 const std::vector<char> &peer, int ndev) {
     nb_builder *own = bs[o];
@@ -411,10 +411,15 @@ int merge_slice(std::vector<nb_builder *> &bs, int o, uint64_t lo, uint64_t len,
             rc = nb_internal_fail(NB_ERR_HIP, "hipMalloc of the merge staging buffer failed");
             break;
         }
-        const hipError_t e = hipMemcpyPeer(tmp + staged * len, dev, bs[s]->ss->d_words + lo, sdev,
-                                           len * 8);  // blocking: complete on return
+        // on the owner's stream, so the OR kernel below is ordered after it.  The
+        // blocking hipMemcpyPeer is NOT: a device-to-device copy returns before it
+        // lands and runs on the null stream, which the slot sets' non-blocking
+        // streams do not wait for (tools/peer_copy_order.hip: stale slices in 32 of
+        // 240 trials vs 0 of 240 on the stream)
+        const hipError_t e = hipMemcpyPeerAsync(tmp + staged * len, dev, bs[s]->ss->d_words + lo,
+                                                sdev, len * 8, st);
         if (e != hipSuccess)
-            rc = nb_internal_fail(NB_ERR_HIP, (std::string("hipMemcpyPeer: ") + hipGetErrorString(e)).c_str());
+            rc = nb_internal_fail(NB_ERR_HIP, (std::string("hipMemcpyPeerAsync: ") + hipGetErrorString(e)).c_str());
         else
             srcs.push_back(tmp + (staged++) * len);
     }

@@ -145,9 +145,10 @@ def test_builder_k0_and_errors(dev):
         b.add(b"abc")
         np.testing.assert_array_equal(b.finish()[:16], init)
     with nbm.Builder(0, 3, SEED) as b:  # the reference divides by zero; the ABI refuses
-        b.add(b"abc")
+        with pytest.raises(nbm.NaspBloomError, match="m == 0"):  # at add(), before any build
+            b.add(b"abc")
         with pytest.raises(nbm.NaspBloomError):
-            b.finish()
+            b.add_batch(np.zeros(32, np.uint8), None, 16, 2)
     with pytest.raises(nbm.NaspBloomError):
         nbm.Builder(100, 3, SEED, flavor=7)
 
