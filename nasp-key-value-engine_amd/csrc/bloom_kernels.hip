@@ -282,6 +282,24 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
     return v;
 }
 
+// An LDS word by its absolute byte address (the address space 3 pointer as an
+// integer): the placement handles below carry absolute addresses, so a placement
+// is one shift, one read, one SDWA add and one store.
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ lds_u32 &lds_at(uint32_t a) { return *(lds_u32 *)(size_t)a; }
+__device__ __forceinline__ uint32_t lds_addr(const uint32_t *p) {
+    return (uint32_t)(size_t)(const lds_u32 *)p;
+}
+
+// __syncthreads_or without the runtime's helper, whose static LDS (256 B) would
+// offset every dynamic-LDS address and cost an add per placement store: `flag` is
+// an LDS word zeroed before an earlier barrier.
+__device__ __forceinline__ bool block_any(int pred, uint32_t *flag) {
+    if (pred) *flag = 1u;
+    __syncthreads();
+    return *flag != 0u;
+}
+
 // Exclusive scan of hist[0..T) into S[0..T); returns the total.  blockDim = NT.
 template <int NT>
 __device__ uint32_t block_exclusive_scan(const uint32_t *hist, uint32_t *S, uint32_t T,
@@ -331,41 +349,52 @@ struct TileScratch {
 // Phases 2-4 of the bin kernel in rank mode when T <= 2 NT: thread tid owns the
 // two tiles 2 tid, 2 tid + 1 from the scan to the run table, so the scan is one
 // wave-scan round (no per-thread loops) and the reservations use the counts it
-// already holds.  Addresses are precomputed where the hot loops use them: the run
-// starts as byte offsets of `sorted` (placement = one shift-add per index) and the
-// run table as byte offsets into the buckets (write-out = one add per entry, a
-// 32-bit offset from the buckets' base) while the buckets stay under 4 GiB.
+// already holds; waves that own no tile skip the scan arithmetic.  The count
+// atomics of phase 1 returned placement handles pk = (4 t) << 16 | 4 rank (see
+// the kernel), so the run starts go over the counters themselves -- as byte
+// offsets of the sort area from `lds` -- and placement is one LDS read of
+// cnt[t] and one add (plus the store).  The run table goes over S: byte offsets
+// into the buckets (write-out = one add and one 32-bit-offset store per word)
+// while the buckets stay under 4 GiB.
 template <int NT, int KPT, int KR, typename ENTRY>
 __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_off_words,
                                                    const TileCfg &tc, const TileScratch &sc,
                                                    ENTRY *__restrict__ buckets, uint64_t base,
                                                    uint64_t n, uint32_t k,
                                                    const uint32_t (&ridx)[KPT][KR],
-                                                   const uint32_t (&rank)[KPT][KR]) {
+                                                   const uint32_t (&pk)[KPT][KR]) {
     constexpr uint32_t kWaves = NT / 64;
     const uint32_t T = tc.T, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    uint32_t *cnt = lds;                  // [T] counts; then the run table
-    uint32_t *S4 = lds + T;               // [T] run starts, byte offsets from lds
+    uint32_t *cnt = lds;                  // [T] packed counters; run starts; limits
+    uint32_t *GX = lds + T;               // [T] run table
     uint32_t *wave_sums = lds + 2 * T;    // [kWaves + 1]
-    char *lds_b = reinterpret_cast<char *>(lds);
-    const uint32_t sort_b = sort_off_words * 4;
-    // ---- phase 2: scan (one round), reservations
-    const uint32_t t0 = 2 * tid;
-    uint32_t h0 = 0, h1 = 0;
-    if (t0 + 1 < T) {
-        const uint2 hh = *reinterpret_cast<const uint2 *>(cnt + t0);
-        h0 = hh.x;
-        h1 = hh.y;
-    } else if (t0 < T) {
-        h0 = cnt[t0];
-    }
+    const uint32_t lds0 = lds_addr(lds);
+    const uint32_t sort_b = lds0 + sort_off_words * 4;  // absolute LDS byte address
     // packed entries (ENTRY = u64, 3 in-tile offsets per word): every run takes a
     // whole number of words, its 1-2 pad slots hold copies of its first entry
     constexpr bool PACK = sizeof(ENTRY) == 8;
     auto slots = [](uint32_t c) { return PACK ? (c + 2) / 3 * 3 : c; };
-    const uint32_t local = slots(h0) + slots(h1);
-    const uint32_t incl = wave_inclusive_scan(local);
+    auto count_of = [&](uint32_t t) { return (cnt[t] - ((lds0 + 4 * t) << 16)) >> 2; };
+    // ---- phase 2: scan (one round), reservations
+    const uint32_t t0 = 2 * tid;
+    const bool scan_wave = wid * 128 < T;  // wave-uniform: the wave owns a tile
+    uint32_t h0 = 0, h1 = 0, incl = 0, local = 0;
+    if (scan_wave) {
+        if (t0 < T) h0 = count_of(t0);
+        if (t0 + 1 < T) h1 = count_of(t0 + 1);
+        local = slots(h0) + slots(h1);
+        incl = wave_inclusive_scan(local);
+    }
     if (lane == 63) wave_sums[wid] = incl;
+    // reservations on tiles tid and tid + NT: a wave's atomics then hit 64
+    // consecutive cursors (4 lines) instead of 128 at stride 2 -- each device-scope
+    // atomic line is a memory-side request (WRITE_SIZE measured 57 vs 30 MB/build)
+    const uint32_t ta = tid, tb = tid + NT;
+    uint32_t ha = 0, hb = 0;
+    if (wid * 64 < T) {  // wave-uniform
+        if (ta < T) ha = count_of(ta);
+        if (tb < T) hb = count_of(tb);
+    }
     __syncthreads();
     if (wid == 0) {
         const uint32_t w = lane < kWaves ? wave_sums[lane] : 0;
@@ -373,21 +402,21 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
         if (lane < kWaves) wave_sums[lane] = wi - w;
         if (lane == kWaves - 1) wave_sums[kWaves] = wi;
     }
-    __syncthreads();
-    const uint32_t st0 = wave_sums[wid] + incl - local, st1 = st0 + slots(h0);
-    const uint32_t total = wave_sums[kWaves];
-    const uint32_t shard = blockIdx.x % tc.G;
+    const uint32_t shard = blockIdx.x & (tc.G - 1);  // G is a power of two
     uint32_t *cur = sc.gcur + (size_t)shard * T;
-    // reservations on tiles tid and tid + NT: a wave's atomics then hit 64
-    // consecutive cursors (4 lines) instead of 128 at stride 2 -- each device-scope
-    // atomic line is a memory-side request (WRITE_SIZE measured 57 vs 30 MB/build)
-    const uint32_t ta = tid, tb = tid + NT;
-    const uint32_t ha = ta < T ? cnt[ta] : 0u, hb = tb < T ? cnt[tb] : 0u;
     const uint32_t ua = PACK ? (ha + 2) / 3 : ha, ub = PACK ? (hb + 2) / 3 : hb;  // bucket units
-    const uint32_t ga = ua ? atomicAdd(&cur[ta], ua) : 0u;
-    const uint32_t gb = ub ? atomicAdd(&cur[tb], ub) : 0u;
-    if (t0 < T) S4[t0] = sort_b + 4 * st0;  // (S4 + t0 is 8-byte aligned only for even T)
-    if (t0 + 1 < T) S4[t0 + 1] = sort_b + 4 * st1;
+    uint32_t ga = 0, gb = 0;
+    if (wid * 64 < T) {  // wave-uniform
+        if (ua) ga = atomicAdd(&cur[ta], ua);
+        if (ub) gb = atomicAdd(&cur[tb], ub);
+    }
+    __syncthreads();  // wave offsets ready; every count has been read
+    const uint32_t total = wave_sums[kWaves];
+    if (scan_wave) {
+        const uint32_t st0 = wave_sums[wid] + incl - local, st1 = st0 + slots(h0);
+        if (t0 < T) cnt[t0] = sort_b + 4 * st0;
+        if (t0 + 1 < T) cnt[t0 + 1] = sort_b + 4 * st1;
+    }
     __syncthreads();
     if (NB_DIAG_STOP(2)) return;
     // ---- phase 3: placement (the reservations' round trips overlap it)
@@ -396,42 +425,44 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
         if (base + (uint64_t)p * NT + tid < n) {
 #pragma unroll
             for (int j = 0; j < KR; ++j)
-                if (j < (int)k)
-                    *reinterpret_cast<uint32_t *>(lds_b + S4[ridx[p][j] >> tc.ts] + 4 * rank[p][j]) =
-                        ridx[p][j];
+                if (j < (int)k) {
+                    const uint32_t h = pk[p][j];
+                    lds_at(lds_at(h >> 16) + (h & 0xffffu)) = ridx[p][j];
+                }
         }
     }
     const int ovf = ((uint64_t)ga + ua > tc.cap) | ((uint64_t)gb + ub > tc.cap);
-    const bool any_ovf = __syncthreads_or(ovf) != 0;  // cnt and S4 are dead now
+    const bool any_ovf = block_any(ovf, wave_sums + kWaves + 1);
     // run table: first-entry index minus the run's local start (wrapping u32), in
-    // bytes when the buckets fit 32-bit offsets; limits over S4 on overflow
+    // bytes when the buckets fit 32-bit offsets; limits over the run starts on
+    // overflow.  (packed: st and the table in words; the pad slots are filled here
+    // -- the placement is complete, and nothing else touches the sort area until
+    // phase 4)
     const bool b32 = (uint64_t)T * tc.G * tc.cap * sizeof(ENTRY) <= 0xFFFFFFFFull;
     const uint32_t esz = (b32 && !any_ovf) ? (uint32_t)sizeof(ENTRY) : 1u;
-    // (packed: st and the table in words; the pad slots are filled here -- the
-    // placement is complete, and nothing else touches the sort area until phase 4)
     auto run_entry = [&](uint32_t t, uint32_t g, uint32_t h) {
-        uint32_t st = (S4[t] - sort_b) / 4;
+        uint32_t st = (cnt[t] - sort_b) / 4;
         if (PACK) {
             uint32_t *run = lds + sort_off_words + st;
             for (uint32_t r = h; r < slots(h); ++r) run[r] = run[0];
             st /= 3;
         }
-        cnt[t] = ((t * tc.G + shard) * tc.cap + g - st) * esz;
+        GX[t] = ((t * tc.G + shard) * tc.cap + g - st) * esz;
         return st;
     };
     uint32_t sa = 0, sbb = 0;
     if (ta < T) sa = run_entry(ta, ga, ha);
     if (tb < T) sbb = run_entry(tb, gb, hb);
     if (any_ovf) {
-        __syncthreads();  // every thread has read S4 before limits go over it
-        if (ta < T) S4[ta] = sa + (ga < tc.cap ? tc.cap - ga : 0u);
-        if (tb < T) S4[tb] = sbb + (gb < tc.cap ? tc.cap - gb : 0u);
+        __syncthreads();  // every thread has read the run starts before limits go over them
+        if (ta < T) cnt[ta] = sa + (ga < tc.cap ? tc.cap - ga : 0u);
+        if (tb < T) cnt[tb] = sbb + (gb < tc.cap ? tc.cap - gb : 0u);
     }
     __syncthreads();
     if (NB_DIAG_STOP(3)) return;
     // ---- phase 4: coalesced write-out, four independent entries per lane per step
     const uint32_t *sorted = lds + sort_off_words;
-    const uint32_t *GX = cnt;
+    const uint32_t *S4 = cnt;  // limits (overflow only)
     if constexpr (PACK) {
         // word q of the block = slots 3q..3q+2 (one run, tile of the first slot)
         const uint32_t words = total / 3, msk = (1u << tc.ts) - 1;
@@ -547,7 +578,15 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     uint32_t *sorted = lds + bin_sort_offset_words(T);  // [KPB * k], 16-byte aligned
     const uint32_t tid = threadIdx.x;
     NB_DIAG_PROLOGUE();
-    for (uint32_t t = tid; t < T; t += NT) cnt[t] = 0;
+    // rank mode (KR > 0): cnt[t] starts at A_t << 16, A_t = the LDS byte address of
+    // cnt[t], and each index adds 4, so the count atomic returns its index's
+    // placement handle pk = A_t << 16 | 4 rank: where the run start will be (the
+    // scan writes it over cnt[t], as an absolute address) and the index's byte
+    // offset within the run.  4 rank <= 4 (2^14 - 1) stays in the low half; a full
+    // count of 2^14 carries into the high half, which the decode
+    // (cnt[t] - (A_t << 16)) >> 2 undoes.
+    for (uint32_t t = tid; t < T; t += NT) cnt[t] = KR > 0 ? lds_addr(cnt + t) << 16 : 0u;
+    if (tid == 0) wave_sums[NT / 64 + 1] = 0u;  // block_any's flag
     __syncthreads();
 
     // phase 1: hash each key once; count its k indices per tile.  With KR > 0
@@ -568,7 +607,7 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
                 if (j < (int)c.k) {
                     if (j) g.next(c);
                     ridx[p][j] = g.r;
-                    rank[p][j] = NB_DIAG_NOCOUNT ? g.r : atomicAdd(&cnt[g.r >> tc.ts], 1u);
+                    rank[p][j] = NB_DIAG_NOCOUNT ? g.r : atomicAdd(&cnt[g.r >> tc.ts], 4u);
                 }
             }
         } else {
@@ -686,8 +725,12 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     // the write-out needs only two words afterwards: G[t] := global entry index of
     // the block's run minus S[t] (u32 wrap-around arithmetic), S[t] := first local
     // position past the bucket's capacity.
+    if (KR > 0) {  // packed counters (see phase 1) back to counts
+        for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << 16)) >> 2;
+        __syncthreads();
+    }
     const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
-    const uint32_t shard = blockIdx.x % tc.G;
+    const uint32_t shard = blockIdx.x & (tc.G - 1);
     uint32_t *cur = sc.gcur + (size_t)shard * T;
     // tiles owned by this thread in phase 2: t = tid + u*NT
     constexpr int kTPT = (kMaxTiles + NT - 1) / NT;
@@ -718,7 +761,8 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
             if (i < n) {
 #pragma unroll
                 for (int j = 0; j < kR; ++j)
-                    if (j < (int)c.k) sorted[S[ridx[p][j] >> tc.ts] + rank[p][j]] = ridx[p][j];
+                    if (j < (int)c.k)
+                        sorted[S[ridx[p][j] >> tc.ts] + ((rank[p][j] & 0xffffu) >> 2)] = ridx[p][j];
             }
         }
 #pragma unroll
@@ -766,7 +810,7 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     // cnt and S are dead: the run table goes over them.  Every run fits its bucket
     // unless the input is pathological (massively duplicated keys): then the
     // table holds {G, limit} pairs and the write-out checks each entry.
-    const bool any_ovf = __syncthreads_or(ovf) != 0;  // block-uniform
+    const bool any_ovf = block_any(ovf, wave_sums + NT / 64 + 1);  // block-uniform
     uint32_t *GX = lds;  // [T] G only, when nothing overflows
 #pragma unroll
     for (int u = 0; u < kTPT; ++u) {
@@ -892,7 +936,7 @@ __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
         const uint32_t incl = wave_inclusive_scan(sl), st = incl - sl;
         if (tid == kSuperFine - 1) slot_total = incl;
         const uint32_t t = fbase + tid;
-        const uint32_t shard = (blockIdx.y * gridDim.x + blockIdx.x) % t2.G;
+        const uint32_t shard = (blockIdx.y * gridDim.x + blockIdx.x) & (t2.G - 1);
         const uint32_t gr = u ? atomicAdd(&sc2.gcur[(size_t)shard * t2.T + t], u) : 0u;
         const uint32_t stu = PACK ? st / 3 : st;
         fS[tid] = st;
@@ -1218,7 +1262,9 @@ TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     ts = std::min<uint32_t>(std::max<uint32_t>(env_u32("NB_TILE_BITS", ts), 12), 20);
     tc.ts = ts;
     tc.T = (uint32_t)(((uint64_t)m + (1ull << ts) - 1) >> ts);
+    // cursor shards: a power of two (the kernels pick a block's shard with a mask)
     tc.G = std::min<uint32_t>(std::max<uint32_t>(env_u32("NB_SHARDS", kShards), 1), kShards);
+    while (tc.G & (tc.G - 1)) tc.G &= tc.G - 1;
     const double e = (double)n_chunk * k / ((double)tc.T * tc.G);
     uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
     cap = (cap + 7) & ~7ull;
@@ -1511,6 +1557,7 @@ int launch_build(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
     }
     FilterConsts c = nb::make_consts(m, k, seed, (uint32_t)flavor);
     if (!offsets) nb::set_fixed_len(c, key_len);
+    if (env_u32("NB_FPMOD", 1) == 0) c.fm.fp = 0;  // A/B: integer remainders only
     g_device_builds.fetch_add(1, std::memory_order_relaxed);
     return flavor == NB_FLAVOR_MSVC_FNV1A
                ? launch_build_f<NB_FLAVOR_MSVC_FNV1A>(keys, offsets, key_len, n, c, words,
@@ -1529,6 +1576,7 @@ int launch_probe(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
     }
     FilterConsts c = nb::make_consts(m, k, seed, (uint32_t)flavor);
     if (!offsets) nb::set_fixed_len(c, key_len);
+    if (env_u32("NB_FPMOD", 1) == 0) c.fm.fp = 0;
     return flavor == NB_FLAVOR_MSVC_FNV1A
                ? launch_probe_f<NB_FLAVOR_MSVC_FNV1A>(keys, offsets, key_len, n, c, words, out, st)
                : launch_probe_f<NB_FLAVOR_LIBSTDCXX>(keys, offsets, key_len, n, c, words, out, st);

@@ -59,9 +59,15 @@ struct FastMod {
     uint32_t l;   // clz32(m)
     uint32_t d;   // m << l (top bit set)
     uint32_t v;   // floor((2^64-1)/d) - 2^32
+    uint32_t fp;  // quotient through f64 (mod64 below): 0 off (m < 2^13),
+                  // 1 for 2^13 <= m < 2^31, 2 for m >= 2^31
+    uint32_t pad_;
+    double inv;   // 1/m, correctly rounded
 };
 
-inline FastMod make_fastmod(uint32_t m) {
+// fp_min: smallest m the f64 quotient is used for (>= 2^13; larger values, or
+// ~0u, keep the integer remainder -- an A/B knob of the kernels' launcher).
+inline FastMod make_fastmod(uint32_t m, uint32_t fp_min = 8192u) {
     FastMod f;
     f.m = m;
     uint32_t l = 0;
@@ -69,6 +75,9 @@ inline FastMod make_fastmod(uint32_t m) {
     f.l = l;
     f.d = m << l;
     f.v = (uint32_t)(~0ULL / f.d - (1ULL << 32));
+    f.fp = (m >= 8192u && m >= fp_min) ? (m < 0x80000000u ? 1u : 2u) : 0u;
+    f.pad_ = 0;
+    f.inv = 1.0 / (double)m;
     return f;
 }
 
@@ -84,12 +93,37 @@ NB_HD uint32_t rem_2by1(uint32_t u1, uint32_t u0, uint32_t d, uint32_t v) {
     return r;
 }
 
-NB_HD uint32_t mod64(uint64_t x, const FastMod &f) {
+NB_HD uint32_t mod64_int(uint64_t x, const FastMod &f) {
     uint32_t n2 = f.l ? (uint32_t)(x >> (64 - f.l)) : 0u;
     uint64_t xs = x << f.l;
     uint32_t r = rem_2by1(n2, (uint32_t)(xs >> 32), f.d, f.v);
     r = rem_2by1(r, (uint32_t)xs, f.d, f.v);
     return r >> f.l;
+}
+
+// x mod m through an f64 quotient (f.fp != 0, m >= 2^13; FMA and conversions are
+// full rate on gfx950): xd = fl(x) is within 2^10 of x, and
+// t = fl(xd * fl(1/m) + 2^52) holds q = rne(xd / m (1 + 2^-53)) in its low mantissa
+// bits, with |q - x/m| < 2^10/m + (x/m) 2^-53 + 1/2 <= 3/8 + 1/2 < 1 (x/m < 2^51), so
+// q = floor(x/m) or one more and x - q m lies in [-m, m).  m < 2^31: that fits a
+// 32-bit two's complement value, corrected by one min (r + m < 2^32 when r >= 0,
+// and wraps below r when r < 0).  m >= 2^31: the 64-bit difference, whose high
+// word is 0 or ~0 (q < 2^52 from bits 0..51).  About 8 / 12 VALU instead of ~26.
+NB_HD uint32_t mod64(uint64_t x, const FastMod &f) {
+    if (f.fp) {  // kernel-uniform
+        const double xd = __builtin_fma((double)(uint32_t)(x >> 32), 4294967296.0,
+                                        (double)(uint32_t)x);
+        const uint64_t tb = __builtin_bit_cast(uint64_t, __builtin_fma(xd, f.inv, 4503599627370496.0));
+        const uint32_t ql = (uint32_t)tb;
+        if (f.fp == 1) {
+            const uint32_t r = (uint32_t)x - ql * f.m, u = r + f.m;
+            return r < u ? r : u;
+        }
+        const uint32_t qh = (uint32_t)(tb >> 32) & 0xFFFFFu;
+        const uint64_t r = x - ((uint64_t)ql * f.m + ((uint64_t)(qh * f.m) << 32));
+        return (uint32_t)r + ((uint32_t)(r >> 32) & f.m);
+    }
+    return mod64_int(x, f);
 }
 
 // (a + b) mod m for a, b < m without 32-bit overflow.

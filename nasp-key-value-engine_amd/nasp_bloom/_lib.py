@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "build", "libnasp_bloom.so")
+# NB_LIB: another build of the same library (same-box A/B of kernel variants)
+LIB_PATH = os.environ.get("NB_LIB") or os.path.join(PKG_ROOT, "build", "libnasp_bloom.so")
 
 NB_OK = 0
 NB_ERR_ARG = -1

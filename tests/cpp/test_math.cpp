@@ -18,12 +18,26 @@ int main() {
                                 1492685679u, 2147483648u, 2147483659u, 3000000019u,
                                 4294967288u, 4294967295u};
     for (int t = 0; t < 2000; ++t) ms.push_back((uint32_t)(rng() >> (rng() % 32)) | 1u);
+    for (uint32_t v : {8191u, 8192u, 8193u, 12289u, 65537u, 2147483647u, 2147483649u, 4294967291u})
+        ms.push_back(v);
     for (uint32_t m : ms) {
-        nb::FastMod f = nb::make_fastmod(m);
-        for (int t = 0; t < 2000; ++t) {
-            uint64_t x = rng();
-            if (t < 8) x = t < 4 ? (uint64_t)t : ~0ull - (uint64_t)(t - 4);
-            if (nb::mod64(x, f) != (uint32_t)(x % m)) ++bad;
+        // the default (f64 quotient from m >= 2^13) and the integer remainder only
+        for (uint32_t fp_min : {8192u, ~0u}) {
+            nb::FastMod f = nb::make_fastmod(m, fp_min);
+            for (int t = 0; t < 4000; ++t) {
+                uint64_t x = rng();
+                if (t < 8) x = t < 4 ? (uint64_t)t : ~0ull - (uint64_t)(t - 4);
+                if (t >= 2000) {
+                    // x = q m + r with r at the ends and the middle of [0, m): the
+                    // quotient estimate's rounding boundaries, up to q = floor(2^64-1 / m)
+                    const uint64_t qmax = ~0ull / m;
+                    const uint64_t q = t < 2100 ? qmax - (uint64_t)(t - 2000) : (qmax == ~0ull ? rng() : rng() % (qmax + 1));
+                    const uint32_t rs[] = {0u, 1u, m - 1, m / 2, m / 2 + 1, m / 2 - 1 + (m == 1)};
+                    x = q * m + rs[t % 6] % m;
+                    if (x / m != q) x = q * m;  // past 2^64 - 1
+                }
+                if (nb::mod64(x, f) != (uint32_t)(x % m)) ++bad;
+            }
         }
         // incremental indices vs direct
         nb::FilterConsts c = nb::make_consts(m, 10, 17027509906831645879ull, 0);

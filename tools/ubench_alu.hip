@@ -73,6 +73,43 @@ __global__ __launch_bounds__(256) void k_lsx_round(uint32_t *out, uint32_t seed)
               x[c] = (x[c] ^ d) * 0xc6a4a7935bd1e995ull; }))
 }
 
+// f64 path of a 64-by-32 remainder (bloom_math.h mod64_f64): conversions and FMAs
+__global__ __launch_bounds__(256) void k_cvt_f64(uint32_t *out, uint32_t seed) {
+    double d[kChains];
+    const uint32_t y = seed | 1u;
+    for (int i = 0; i < kIters; ++i) {
+        _Pragma("unroll") for (int c = 0; c < kChains; ++c)
+            asm volatile("v_cvt_f64_u32 %0, %1" : "=v"(d[c]) : "v"(y + c));
+    }
+    double acc = 0;
+    for (int c = 0; c < kChains; ++c) acc += d[c];
+    if (acc == 1.5) out[blockIdx.x] = 1;
+}
+__global__ __launch_bounds__(256) void k_fma64(uint32_t *out, uint32_t seed) {
+    double d[kChains];
+    for (int c = 0; c < kChains; ++c) d[c] = threadIdx.x * 0.5 + c + seed;
+    const double y = 1.0000001, z = 0.25;
+    for (int i = 0; i < kIters; ++i) {
+        _Pragma("unroll") for (int c = 0; c < kChains; ++c)
+            asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(d[c]) : "v"(y), "v"(z));
+    }
+    double acc = 0;
+    for (int c = 0; c < kChains; ++c) acc += d[c];
+    if (acc == 1.5) out[blockIdx.x] = 1;
+}
+// 64-bit multiply by a constant as three v_mad_u64_u32 (low product, then the two
+// cross products accumulated into the high half)
+__device__ __forceinline__ uint64_t mul64_mad3(uint64_t x, uint64_t k) {
+    uint64_t p, q, r;
+    asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, 0" : "=v"(p) : "v"((uint32_t)x), "v"((uint32_t)k) : "vcc");
+    asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(q) : "v"((uint32_t)(x >> 32)), "v"((uint32_t)k), "v"(p >> 32) : "vcc");
+    asm volatile("v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=v"(r) : "v"((uint32_t)x), "v"((uint32_t)(k >> 32)), "v"(q) : "vcc");
+    return (p & 0xffffffffull) | (r << 32);
+}
+__global__ __launch_bounds__(256) void k_mul64_mad3(uint32_t *out, uint32_t seed) {
+    BODY64(x[c] = mul64_mad3(x[c], y64))
+}
+
 template <class K>
 static void run(const char *name, K kern, double ops_per_iter_chain) {
     uint32_t *out;
@@ -113,5 +150,8 @@ int main() {
     run("lshr64", k_lshr64, 1);
     run("mul64xC", k_mul64_c, 1);    // ops = 64-bit multiplies
     run("lsx_round", k_lsx_round, 1);  // ops = hash rounds
+    run("cvt_f64_u32", k_cvt_f64, 1);
+    run("fma_f64", k_fma64, 1);
+    run("mul64_mad3", k_mul64_mad3, 1);  // ops = 64-bit multiplies
     return 0;
 }

@@ -23,6 +23,7 @@ __constant__ int g_stagger_cycles;
 
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 #define CK(x)                                                               \
     do {                                                                    \
@@ -55,23 +56,38 @@ static void set_stagger(int blocks, int cycles) {
 
 static size_t g_lds_pad = 0;  // extra dynamic LDS (forces fewer blocks per CU)
 
-template <int KPT, typename E, int KR = 0>
-static float time_bin(const uint8_t *keys, uint64_t n, const FilterConsts &c, TileCfg tc,
-                      TileScratch sc, void *buckets, int stop) {
+// The product's C2 configuration: choose_tiles + the packed-entry capacity of
+// launch_tiled (three 21-bit in-tile offsets per 64-bit word).
+static TileCfg c2_tiles(uint64_t n, uint32_t m, uint32_t k) {
+    TileCfg tc = choose_tiles(m, n, k);
+    constexpr uint64_t kpb = (uint64_t)kBinKPT * kBinThreads;
+    const uint64_t nblk = (n + kpb - 1) / kpb, bps = (nblk + tc.G - 1) / tc.G;
+    const uint64_t capw = ((uint64_t)tc.cap + 2 * bps + 2) / 3;
+    tc.cap = (uint32_t)((capw + 7) & ~7ull);
+    return tc;
+}
+
+static const uint64_t *g_offsets = nullptr;  // set: variable-length keys (C3)
+
+template <int KPT, typename E, int KR>
+static float time_bin_packed(const uint8_t *keys, uint64_t n, const FilterConsts &c, TileCfg tc,
+                             TileScratch sc, void *buckets, int stop) {
     constexpr int NT = kBinThreads;
     constexpr uint64_t kpb = (uint64_t)KPT * NT;
-    const size_t lds = (size_t)bin_sort_offset_words(tc.T) * 4 + kpb * c.k * 4 + g_lds_pad;
-    auto kern = bloom_bin_kernel<0, kFixed16, KPT, E, NT, false, KR>;
-    if (lds > 160 * 1024) return -1.f;
+    size_t sort = kpb * c.k * 4 + (size_t)tc.T * 8;
+    if (g_offsets) sort = std::max<size_t>(sort, stage_lds_bytes(NT));
+    const size_t lds = (size_t)bin_sort_offset_words(tc.T) * 4 + sort + g_lds_pad;
+    auto kern = g_offsets ? bloom_bin_kernel<0, kOffsets, KPT, E, NT, true, KR>
+                          : bloom_bin_kernel<0, kFixed16, KPT, E, NT, false, KR>;
     allow_lds(kern, lds);
     set_stop(stop);
     Ev ev;
     float best = 1e30f;
-    for (int r = 0; r < 3; ++r) {
+    for (int r = 0; r < 5; ++r) {
         CK(hipMemset(sc.gcur, 0, kCurWords * 4));
         CK(hipEventRecord(ev.a));
         hipLaunchKernelGGL(kern, dim3((uint32_t)((n + kpb - 1) / kpb)), dim3(NT), lds, 0, keys,
-                           nullptr, 16u, n, c, tc, sc, (E *)buckets);
+                           g_offsets, g_offsets ? 0u : 16u, n, c, tc, sc, (E *)buckets);
         CK(hipEventRecord(ev.b));
         CK(hipEventSynchronize(ev.b));
         float ms;
@@ -82,40 +98,36 @@ static float time_bin(const uint8_t *keys, uint64_t n, const FilterConsts &c, Ti
     return best;
 }
 
-template <typename E, int UN>
-static float time_tile(const uint8_t *keys, uint64_t n, const FilterConsts &c, TileCfg tc,
-                       TileScratch sc, void *buckets, uint64_t *words) {
-    auto kern = bloom_tile_or_kernel<E, true, kTileThreads, UN>;
-    const size_t lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
-    allow_lds(kern, lds);
-    const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
-    Ev ev;
-    float best = 1e30f;
-    for (int r = 0; r < 3; ++r) {
-        time_bin<kBinKPT, E>(keys, n, c, tc, sc, buckets, 0);
-        CK(hipEventRecord(ev.a));
-        hipLaunchKernelGGL(kern, dim3(tc.T), dim3(kTileThreads), lds, 0, tc, sc, (const E *)buckets,
-                           words, nwords);
-        CK(hipEventRecord(ev.b));
-        CK(hipEventSynchronize(ev.b));
-        float ms;
-        CK(hipEventElapsedTime(&ms, ev.a, ev.b));
-        best = std::min(best, ms);
-    }
-    return best;
-}
-
 int main(int argc, char **argv) {
-    const bool pmc = argc > 1 && !strcmp(argv[1], "pmc");  // one dispatch per stop, for counters
-    const uint64_t n = 10000000;
-    const uint32_t m = 95850584, k = 7;
+    // argv[1]: c2 (default), c4 (the 100M-key shard) or c3 (100M keys of 8-64 bytes);
+    // argv[2] == "intmod": integer remainders
+    const bool c4 = argc > 1 && !strcmp(argv[1], "c4"), c3 = argc > 1 && !strcmp(argv[1], "c3");
+    const uint64_t n = (c4 || c3) ? 100000000 : 10000000;
+    const uint32_t m = (c4 || c3) ? 958505838u : 95850584u, k = 7;
     uint8_t *keys;
     uint64_t *words;
-    CK(hipMalloc(&keys, n * 16 + 64));
+    uint64_t key_bytes = n * 16;
+    if (c3) {  // lengths 8 + (splitmix(i) mod 57), offsets by a host scan
+        std::vector<uint64_t> offs(n + 1, 0);
+        for (uint64_t i = 0; i < n; ++i) {
+            uint64_t x = i * 0x9E3779B97F4A7C15ull + 0x1EA5;
+            x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+            x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+            offs[i + 1] = offs[i] + 8 + (x ^ (x >> 31)) % 57;
+        }
+        key_bytes = offs[n];
+        uint64_t *d_offs;
+        CK(hipMalloc(&d_offs, (n + 1) * 8));
+        CK(hipMemcpy(d_offs, offs.data(), (n + 1) * 8, hipMemcpyHostToDevice));
+        g_offsets = d_offs;
+    }
+    CK(hipMalloc(&keys, key_bytes + 64));
     CK(hipMalloc(&words, ((uint64_t)m + 63) / 64 * 8));
-    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint64_t *>(keys), 2 * n);
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint64_t *>(keys),
+                       (key_bytes + 7) / 8);
     FilterConsts c = nb::make_consts(m, k, 17027509906831645879ull, 0);
-    nb::set_fixed_len(c, 16);
+    if (!c3) nb::set_fixed_len(c, 16);
+    if (argc > 2 && !strcmp(argv[2], "intmod")) c.fm.fp = 0;
     void *buckets;
     TileScratch sc;
     uint32_t *zeroed;
@@ -125,74 +137,66 @@ int main(int argc, char **argv) {
     sc.gcur = zeroed;
     sc.spill_flag = zeroed + kCurWords;
     sc.spill32 = zeroed + kCurWords + kMaxTiles;
-    CK(hipMalloc(&buckets, (size_t)n * k * 4 * 2 + (1 << 26)));
-    if (pmc) {
-        TileCfg tc;
-        tc.ts = 16;
-        tc.T = (uint32_t)(((uint64_t)m + (1ull << 16) - 1) >> 16);
-        tc.G = 8;
-        double e = (double)n * k / ((double)tc.T * tc.G);
-        tc.cap = ((uint32_t)(e + 8 * std::sqrt(e) + 64) + 7) & ~7u;
-        constexpr int NT = kBinThreads;
-        constexpr uint64_t kpb = (uint64_t)kBinKPT * NT;
-        const size_t lds = (size_t)bin_sort_offset_words(tc.T) * 4 + kpb * c.k * 4;
-        auto kern = bloom_bin_kernel<0, kFixed16, kBinKPT, uint16_t, NT, false, 8>;
-        allow_lds(kern, lds);
-        // dispatch order: stop 11, 1, 2, 3, 0 (full), then the tile kernel
+    CK(hipMalloc(&buckets, (size_t)n * k * 4 + (1 << 28)));
+    const TileCfg tc = c2_tiles(n, m, k);
+    if (argc > 2 && !strcmp(argv[2], "pmc")) {
+        // one dispatch per stop (11 = hash only, 1 = + count, 2 = + scan/reservations,
+        // 3 = + placement, 0 = full), in that order, for per-phase counters
         for (int stop : {11, 1, 2, 3, 0}) {
             set_stop(stop);
+            constexpr uint64_t kpb = (uint64_t)kBinKPT * kBinThreads;
+            size_t sort = kpb * c.k * 4 + (size_t)tc.T * 8;
+            if (g_offsets) sort = std::max<size_t>(sort, stage_lds_bytes(kBinThreads));
+            const size_t lds = (size_t)bin_sort_offset_words(tc.T) * 4 + sort;
+            auto kern = g_offsets ? bloom_bin_kernel<0, kOffsets, kBinKPT, uint64_t, kBinThreads, true, 8>
+                                  : bloom_bin_kernel<0, kFixed16, kBinKPT, uint64_t, kBinThreads, false, 8>;
+            allow_lds(kern, lds);
             CK(hipMemset(sc.gcur, 0, kCurWords * 4));
-            hipLaunchKernelGGL(kern, dim3((uint32_t)((n + kpb - 1) / kpb)), dim3(NT), lds, 0, keys,
-                               nullptr, 16u, n, c, tc, sc, (uint16_t *)buckets);
+            hipLaunchKernelGGL(kern, dim3((uint32_t)((n + kpb - 1) / kpb)), dim3(kBinThreads), lds, 0,
+                               keys, g_offsets, g_offsets ? 0u : 16u, n, c, tc, sc, (uint64_t *)buckets);
             CK(hipDeviceSynchronize());
         }
         set_stop(0);
-        auto tk = bloom_tile_or_kernel<uint16_t, true>;
-        const size_t tl = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
-        allow_lds(tk, tl);
-        hipLaunchKernelGGL(tk, dim3(tc.T), dim3(kTileThreads), tl, 0, tc, sc, (const uint16_t *)buckets,
-                           words, ((uint64_t)m + 63) / 64);
-        CK(hipDeviceSynchronize());
-        printf("pmc mode done\n");
+        printf("pmc dispatches: stops 11 1 2 3 0\n");
         return 0;
     }
-    {
-        TileCfg tc;
-        tc.ts = 16;
-        tc.T = (uint32_t)(((uint64_t)m + (1ull << 16) - 1) >> 16);
-        tc.G = 8;
-        double e = (double)n * k / ((double)tc.T * tc.G);
-        tc.cap = ((uint32_t)(e + 8 * std::sqrt(e) + 64) + 7) & ~7u;
-        for (size_t pad : {(size_t)0, (size_t)70 * 1024}) {
-            g_lds_pad = pad;
-            printf("ts=16 T=%u G=8 u16 lds_pad=%zu (%s block/CU): p1 %.4f p12 %.4f p123 %.4f full %.4f ms\n",
-                   tc.T, pad, pad ? "1" : "2",
-                   time_bin<kBinKPT, uint16_t>(keys, n, c, tc, sc, buckets, 1),
-                   time_bin<kBinKPT, uint16_t>(keys, n, c, tc, sc, buckets, 2),
-                   time_bin<kBinKPT, uint16_t>(keys, n, c, tc, sc, buckets, 3),
-                   time_bin<kBinKPT, uint16_t>(keys, n, c, tc, sc, buckets, 0));
-        }
-        g_lds_pad = 0;
-        printf("rank mode (KR=8): p1-nocount %.4f p1 %.4f p12 %.4f p123 %.4f full %.4f ms\n",
-               time_bin<kBinKPT, uint16_t, 8>(keys, n, c, tc, sc, buckets, 11),
-               time_bin<kBinKPT, uint16_t, 8>(keys, n, c, tc, sc, buckets, 1),
-               time_bin<kBinKPT, uint16_t, 8>(keys, n, c, tc, sc, buckets, 2),
-               time_bin<kBinKPT, uint16_t, 8>(keys, n, c, tc, sc, buckets, 3),
-               time_bin<kBinKPT, uint16_t, 8>(keys, n, c, tc, sc, buckets, 0));
-        printf("tile kernel: %.4f ms\n", time_tile<uint16_t, kTileUnroll>(keys, n, c, tc, sc, buckets, words));
-        printf("tile kernel unroll 1/4/8: %.4f %.4f %.4f ms\n",
-               time_tile<uint16_t, 1>(keys, n, c, tc, sc, buckets, words),
-               time_tile<uint16_t, 4>(keys, n, c, tc, sc, buckets, words),
-               time_tile<uint16_t, 8>(keys, n, c, tc, sc, buckets, words));
-        // desynchronise the two resident blocks per CU: blocks [lo, 2lo) start late
-        for (int lo : {256, 512})
-            for (int cyc : {4000, 8000, 16000, 24000}) {
-                set_stagger(lo, cyc);
-                printf("stagger lo=%d cycles=%d: full %.4f ms\n", lo, cyc,
-                       time_bin<kBinKPT, uint16_t, 8>(keys, n, c, tc, sc, buckets, 0));
-            }
-        set_stagger(0, 0);
+    printf("%s packed: ts=%u T=%u G=%u cap=%u words\n", c3 ? "C3" : c4 ? "C4" : "C2", tc.ts, tc.T, tc.G, tc.cap);
+    for (size_t pad : {(size_t)0, (size_t)96 * 1024}) {
+        g_lds_pad = pad;
+        printf("%s block/CU: p1-nocount %.4f p1 %.4f p12 %.4f p123 %.4f full %.4f ms\n", pad ? "1" : "2",
+               time_bin_packed<kBinKPT, uint64_t, 8>(keys, n, c, tc, sc, buckets, 11),
+               time_bin_packed<kBinKPT, uint64_t, 8>(keys, n, c, tc, sc, buckets, 1),
+               time_bin_packed<kBinKPT, uint64_t, 8>(keys, n, c, tc, sc, buckets, 2),
+               time_bin_packed<kBinKPT, uint64_t, 8>(keys, n, c, tc, sc, buckets, 3),
+               time_bin_packed<kBinKPT, uint64_t, 8>(keys, n, c, tc, sc, buckets, 0));
     }
+    g_lds_pad = 0;
+    {
+        auto kern = bloom_tile_or_kernel<uint64_t, true>;
+        const size_t lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
+        allow_lds(kern, lds);
+        Ev ev;
+        float best = 1e30f;
+        for (int r = 0; r < 5; ++r) {
+            time_bin_packed<kBinKPT, uint64_t, 8>(keys, n, c, tc, sc, buckets, 0);
+            CK(hipEventRecord(ev.a));
+            hipLaunchKernelGGL(kern, dim3(tc.T), dim3(kTileThreads), lds, 0, tc, sc,
+                               (const uint64_t *)buckets, words, ((uint64_t)m + 63) / 64);
+            CK(hipEventRecord(ev.b));
+            CK(hipEventSynchronize(ev.b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, ev.a, ev.b));
+            best = std::min(best, ms);
+        }
+        printf("tile kernel: %.4f ms\n", best);
+    }
+    for (int lo : {256, 512})
+        for (int cyc : {8000, 30000, 60000}) {
+            set_stagger(lo, cyc);
+            printf("stagger lo=%d cycles=%d: full %.4f ms\n", lo, cyc,
+                   time_bin_packed<kBinKPT, uint64_t, 8>(keys, n, c, tc, sc, buckets, 0));
+        }
+    set_stagger(0, 0);
     CK(hipDeviceSynchronize());
     return 0;
 }
