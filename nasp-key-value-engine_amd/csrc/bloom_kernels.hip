@@ -442,9 +442,14 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     const uint32_t esz = (b32 && !any_ovf) ? (uint32_t)sizeof(ENTRY) : 1u;
     auto run_entry = [&](uint32_t t, uint32_t g, uint32_t h) {
         uint32_t st = (cnt[t] - sort_b) / 4;
-        if (PACK) {
+        if (PACK) {  // 0-2 pad slots (straight-line: the compiler would emit a memset loop)
             uint32_t *run = lds + sort_off_words + st;
-            for (uint32_t r = h; r < slots(h); ++r) run[r] = run[0];
+            const uint32_t np = slots(h) - h;
+            if (np) {
+                const uint32_t v0 = run[0];
+                run[h] = v0;
+                if (np > 1) run[h + 1] = v0;
+            }
             st /= 3;
         }
         GX[t] = ((t * tc.G + shard) * tc.cap + g - st) * esz;
@@ -676,8 +681,11 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
             uint32_t klo = (uint32_t)(b - kb0 + a0), klen = (uint32_t)(e - b);
             bool kvalid = i < n;
             if (kPermute && staged) {
-                // counting sort of the sub-batch by word count (absent keys last)
-                const uint32_t cls = kvalid ? min((klen + 7) >> 3, kLenClasses - 2) : kLenClasses - 1;
+                // counting sort of the sub-batch by word count (absent keys last): whole
+                // words for the libstdc++ dword path (its loop runs over whole words,
+                // then one tail), all words touched for the byte-wise FNV-1a loop
+                const uint32_t nw = FLAVOR == NB_FLAVOR_LIBSTDCXX ? klen >> 3 : (klen + 7) >> 3;
+                const uint32_t cls = kvalid ? min(nw, kLenClasses - 2) : kLenClasses - 1;
                 kinfo[tid] = klo | (klen << 16);  // both < 2^16 inside the stage
                 const uint32_t r = atomicAdd(&lhist[cls], 1u);
                 __syncthreads();
@@ -698,7 +706,18 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
             if (kvalid) {
                 uint64_t h1, h2;
                 const uint32_t len = klen;
-                if (staged) {
+                if (staged && FLAVOR == NB_FLAVOR_LIBSTDCXX) {
+                    // dword stream from LDS (bloom_math.h lsx_hash_dwords); its reads run
+                    // <= 12 bytes past the key, inside the stage's allocation
+                    const uint32_t *dw = reinterpret_cast<const uint32_t *>(stage) + (klo >> 2);
+                    auto D = [dw](uint32_t j) { return dw[j]; };
+                    const uint32_t sh = 8 * (klo & 3u);
+                    const uint64_t g0 =
+                        LAYOUT == kFixedStride ? c.h2_init_fixed : nb::lsx_h2_start(c, len);
+                    if (c.prem == 0) nb::lsx_hash_dwords<0>(c, D, sh, len, g0, &h1, &h2);
+                    else if (c.prem <= 4) nb::lsx_hash_dwords<1>(c, D, sh, len, g0, &h1, &h2);
+                    else nb::lsx_hash_dwords<2>(c, D, sh, len, g0, &h1, &h2);
+                } else if (staged) {
                     const uint32_t lo = klo, a = lo & 7u;
                     const uint64_t *q = reinterpret_cast<const uint64_t *>(stage + (lo - a));
                     auto load = [q](uint32_t j) { return q[j]; };

@@ -335,6 +335,79 @@ NB_HD void hash_aligned_words(const FilterConsts &c, LoadQ Q, uint32_t a, uint32
     }
 }
 
+// ------------------------------------------- dword-stream libstdc++ path ----
+// The same two hashes for a key read as 32-bit dwords (the LDS-staged keys of the
+// bin kernel): two v_alignbit_b32 per key word instead of a 64-bit funnel shift,
+// no per-word length masks (whole words in the loop, one masked tail after it),
+// and the h2 stream's seed-prefix splice as two more alignbits with a
+// kernel-uniform shift (prefix class PC: 0 for D % 8 == 0, 1 for 1..4, 2 for 5..7).
+
+// ({hi, lo} >> (s & 31))[31:0]: v_alignbit_b32 on the device.
+NB_HD uint32_t alignbit(uint32_t hi, uint32_t lo, uint32_t s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbit(hi, lo, s);
+#else
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (s & 31));
+#endif
+}
+NB_HD uint64_t pack64(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
+
+// Stream word = the previous key word's top p bytes ++ this key word's low 8 - p
+// bytes, i.e. ({kw, kwp} >> (64 - 8p))[63:0] (p = D % 8, uniform).
+template <int PC>
+NB_HD uint64_t lsx_splice(uint64_t kwp, uint64_t kw, uint32_t p) {
+    const uint32_t pl = (uint32_t)kwp, ph = (uint32_t)(kwp >> 32);
+    const uint32_t l = (uint32_t)kw, h = (uint32_t)(kw >> 32);
+    if (PC == 0) return kw;
+    if (PC == 1) return pack64(alignbit(l, ph, 32 - 8 * p), alignbit(h, l, 32 - 8 * p));
+    return pack64(alignbit(ph, pl, 64 - 8 * p), alignbit(l, ph, 64 - 8 * p));
+}
+
+// h1 = H(key), h2 = H(to_string(seed) ++ key) for a key of len bytes starting at
+// bit sh (0, 8, 16, 24) of dword D(0); D(i) returns dword i, and reads run up to
+// 12 bytes past the key's last byte.  g0: h2's state after the whole prefix words
+// (lsx_init(len + D) mixed with pre_d, or c.h2_init_fixed for fixed-length keys).
+template <int PC, class LoadD>
+NB_HD void lsx_hash_dwords(const FilterConsts &c, LoadD D, uint32_t sh, uint32_t len, uint64_t g0,
+                           uint64_t *h1o, uint64_t *h2o) {
+    const uint32_t L8 = len >> 3, rem = len & 7, p = c.prem;
+    auto mask = [](uint64_t x, uint32_t nb) { return x & ((1ull << (8 * nb)) - 1); };
+    uint64_t h = lsx_init(len), g = g0;
+    uint64_t kwp = PC ? c.pre_tail << (64 - 8 * p) : 0;  // key word -1 as the splice sees it
+    uint32_t d0 = D(0), d1 = D(1);
+    for (uint32_t j = 0; j < L8; ++j) {  // whole key words and whole stream words
+        const uint32_t d2 = D(2 * j + 2), d3 = D(2 * j + 3);
+        const uint64_t kw = pack64(alignbit(d1, d0, sh), alignbit(d2, d1, sh));
+        h = lsx_round(h, kw);
+        g = lsx_round(g, lsx_splice<PC>(kwp, kw, p));
+        kwp = kw;
+        d0 = d2;
+        d1 = d3;
+    }
+    // key word L8 (its first rem bytes are the key's; the rest is read past it)
+    const uint64_t kwt = pack64(alignbit(d1, d0, sh), alignbit(D(2 * L8 + 2), d1, sh));
+    if (rem) h = lsx_tail(h, mask(kwt, rem));
+    // stream word L8 holds p + rem valid bytes: a whole round when that reaches 8,
+    // then word L8 + 1 holds the rest (p + rem - 8, from kwt alone)
+    const uint32_t sv = p + rem;
+    if (sv >= 8) {
+        g = lsx_round(g, lsx_splice<PC>(kwp, kwt, p));
+        if (sv > 8) g = lsx_tail(g, mask(lsx_splice<PC>(kwt, 0, p), sv - 8));
+    } else if (sv) {
+        g = lsx_tail(g, mask(lsx_splice<PC>(kwp, kwt, p), sv));
+    }
+    *h1o = lsx_final(h);
+    *h2o = lsx_final(g);
+}
+
+// g0 for a variable-length key (lsx_begin's h2 state).
+NB_HD uint64_t lsx_h2_start(const FilterConsts &c, uint32_t len) {
+    uint64_t g = lsx_init((uint64_t)len + c.plen);
+    for (int w = 0; w < kMaxPrefixWords; ++w)
+        if ((uint32_t)w < c.pwords) g = (g ^ c.pre_d[w]) * kMul;
+    return g;
+}
+
 // ------------------------------------------------------------- Merkle ----
 // MerkleTree (reference MerkleTree/merkle.cpp:7-55) hashes with the same
 // std::hash<std::string> as the filter, over decimal strings: a leaf is

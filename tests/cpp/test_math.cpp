@@ -62,7 +62,10 @@ int main() {
     printf("mod/incremental mismatches: %ld\n", bad);
     long hbad = 0;
     uint64_t seeds[] = {0ull, 5ull, 12345678ull, 123456789ull, 1234567890123456ull,
-                        17027509906831645879ull, 18446744073709551615ull, 99999999ull};
+                        17027509906831645879ull, 18446744073709551615ull, 99999999ull,
+                        // D % 8 = 2, 3, 5, 6, 7 (every prefix class of the dword path)
+                        12ull, 123ull, 1234567890123ull, 12345678901234ull, 123456789012345ull,
+                        1234567ull};
     for (uint64_t seed : seeds) {
         for (int fl = 0; fl < 2; ++fl) {
             nb::FilterConsts c = nb::make_consts(1000003u, 7, seed, (uint32_t)fl);
@@ -90,6 +93,24 @@ int main() {
                     nb::hash_aligned_words<0, decltype(load), true>(cf, load, a, (uint32_t)len,
                                                                     &g1, &g2);
                     if (g1 != h1 || g2 != h2) ++hbad;
+                }
+                if (fl == 0) {
+                    // the dword-stream path of the staged bin kernel (prefix class of
+                    // D % 8), key at byte offset 0..3 of a dword, junk around it
+                    alignas(4) uint8_t dw[128 + 32];
+                    const uint32_t b = (uint32_t)(rng() % 4);
+                    for (size_t q = 0; q < sizeof dw; ++q) dw[q] = (uint8_t)rng();
+                    for (size_t q = 0; q < len; ++q) dw[b + q] = buf[q];
+                    const uint32_t *d32 = reinterpret_cast<const uint32_t *>(dw);
+                    auto D = [d32](uint32_t i) { return d32[i]; };
+                    const uint32_t pc = c.prem == 0 ? 0 : c.prem <= 4 ? 1 : 2;
+                    for (int fixed = 0; fixed < 2; ++fixed) {
+                        const uint64_t g0 = fixed ? cf.h2_init_fixed : nb::lsx_h2_start(c, (uint32_t)len);
+                        if (pc == 0) nb::lsx_hash_dwords<0>(c, D, 8 * b, (uint32_t)len, g0, &g1, &g2);
+                        else if (pc == 1) nb::lsx_hash_dwords<1>(c, D, 8 * b, (uint32_t)len, g0, &g1, &g2);
+                        else nb::lsx_hash_dwords<2>(c, D, 8 * b, (uint32_t)len, g0, &g1, &g2);
+                        if (g1 != h1 || g2 != h2) ++hbad;
+                    }
                 }
                 for (uint32_t i = 0; i < 3; ++i) {
                     uint32_t want = orc_index(fl, buf, len, i, 1000003u, seed);

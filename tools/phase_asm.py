@@ -18,6 +18,7 @@ def main():
     s = s.replace('#include "bloom_math.h"', f'#include "{CSRC}/bloom_math.h"')
     s = s.replace('#include "../../include/nasp_bloom.h"', f'#include "{REPO}/include/nasp_bloom.h"')
     s = s.replace("    if (NB_DIAG_STOP(1)) return;", '    asm volatile(";NBMARK phase2");\n    if (NB_DIAG_STOP(1)) return;')
+    s = s.replace("    if (NB_DIAG_STOP(2)) return;", '    asm volatile(";NBMARK phase3");\n    if (NB_DIAG_STOP(2)) return;')
     s = s.replace("    if (NB_DIAG_STOP(3)) return;", '    asm volatile(";NBMARK phase4");\n    if (NB_DIAG_STOP(3)) return;')
     os.makedirs("/tmp/nbasm", exist_ok=True)
     open("/tmp/nbasm/k.hip", "w").write(s)
