@@ -36,7 +36,10 @@ size_t nb_internal_frame_header(uint32_t m, uint32_t k, double p, uint32_t time_
 
 namespace {
 
-enum Layout : int { kOffsets = 0, kFixedStride = 1, kFixed16 = 2 };
+// kFixed16 / kFixed32: 16- / 32-byte keys at a 16-byte-aligned base, loaded as
+// dwordx4 vectors straight into registers (no LDS stage)
+enum Layout : int { kOffsets = 0, kFixedStride = 1, kFixed16 = 2, kFixed32 = 3 };
+constexpr bool vec_layout(int l) { return l == kFixed16 || l == kFixed32; }
 
 constexpr int kBlock = 256;
 
@@ -119,35 +122,71 @@ __device__ __forceinline__ void key_hashes_16(const FilterConsts &c, const uint8
     hash16<FLAVOR>(c, reinterpret_cast<const ulonglong2 *>(keys)[i], h1, h2);
 }
 
+// 32-byte keys (C5's shape): four words in registers; h2's stream words are the
+// seed-prefix splice of consecutive key words (bloom_math.h lsx_splice, prefix
+// class PC of D % 8), then the D % 8 leftover bytes as the tail.
+template <int PC>
+__device__ __forceinline__ void lsx32(const FilterConsts &c, const uint64_t (&w)[4], uint64_t *h1,
+                                      uint64_t *h2) {
+    uint64_t h = nb::lsx_init(32), g = c.h2_init_fixed;
+    const uint32_t p = c.prem;
+    uint64_t kwp = PC ? c.pre_tail << (64 - 8 * p) : 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        h = nb::lsx_round(h, w[j]);
+        g = nb::lsx_round(g, nb::lsx_splice<PC>(kwp, w[j], p));
+        kwp = w[j];
+    }
+    if (PC) g = nb::lsx_tail(g, nb::lsx_splice<PC>(kwp, 0, p) & ((1ull << (8 * p)) - 1));
+    *h1 = nb::lsx_final(h);
+    *h2 = nb::lsx_final(g);
+}
+
+template <int FLAVOR>
+__device__ __forceinline__ void hash32(const FilterConsts &c, const ulonglong2 &a,
+                                       const ulonglong2 &b, uint64_t *h1, uint64_t *h2) {
+    const uint64_t w[4] = {a.x, a.y, b.x, b.y};
+    if (FLAVOR == NB_FLAVOR_MSVC_FNV1A) {
+        uint64_t f1 = nb::kFnvBasis, f2 = c.fnv_pre;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) nb::fnv_consume(f1, f2, w[j], 8);
+        *h1 = f1;
+        *h2 = f2;
+    } else if (c.prem == 0) {  // kernel-uniform
+        lsx32<0>(c, w, h1, h2);
+    } else if (c.prem <= 4) {
+        lsx32<1>(c, w, h1, h2);
+    } else {
+        lsx32<2>(c, w, h1, h2);
+    }
+}
+
 // A block's KPT keys per lane: all loads issued before any hashing, so a lane
 // has KPT key loads (fixed 16-byte keys) or offset pairs (variable keys) in
 // flight at once instead of one exposed latency per key.
 template <int FLAVOR, int LAYOUT, int KPT>
 struct KeyBatch {
-    ulonglong2 kv[KPT];
+    ulonglong2 kv[KPT], kv2[LAYOUT == kFixed32 ? KPT : 1];
     uint64_t b[KPT], e[KPT];
-    __device__ __forceinline__ void load(const uint8_t *keys, const uint64_t *offsets,
-                                         uint64_t base, uint64_t stride, uint64_t n) {
-#pragma unroll
-        for (int p = 0; p < KPT; ++p) {
-            const uint64_t i = base + p * stride;
-            if (i < n) {
-                if (LAYOUT == kFixed16) kv[p] = reinterpret_cast<const ulonglong2 *>(keys)[i];
-                else if (LAYOUT == kOffsets) { b[p] = offsets[i]; e[p] = offsets[i + 1]; }
-            }
-        }
-    }
     __device__ __forceinline__ void load_one(int p, const uint8_t *keys, const uint64_t *offsets,
                                              uint64_t i, uint64_t n) {
         if (i < n) {
-            if (LAYOUT == kFixed16) kv[p] = reinterpret_cast<const ulonglong2 *>(keys)[i];
+            const ulonglong2 *kq = reinterpret_cast<const ulonglong2 *>(keys);
+            if (LAYOUT == kFixed16) kv[p] = kq[i];
+            else if (LAYOUT == kFixed32) { kv[p] = kq[2 * i]; kv2[LAYOUT == kFixed32 ? p : 0] = kq[2 * i + 1]; }
             else if (LAYOUT == kOffsets) { b[p] = offsets[i]; e[p] = offsets[i + 1]; }
         }
+    }
+    __device__ __forceinline__ void load(const uint8_t *keys, const uint64_t *offsets,
+                                         uint64_t base, uint64_t stride, uint64_t n) {
+#pragma unroll
+        for (int p = 0; p < KPT; ++p) load_one(p, keys, offsets, base + p * stride, n);
     }
     __device__ __forceinline__ void hash(const FilterConsts &c, const uint8_t *keys,
                                          uint32_t key_len, uint64_t i, int p, uint64_t *h1,
                                          uint64_t *h2) const {
         if (LAYOUT == kFixed16) hash16<FLAVOR>(c, kv[p], h1, h2);
+        else if (LAYOUT == kFixed32) hash32<FLAVOR>(c, kv[p], kv2[LAYOUT == kFixed32 ? p : 0], h1, h2);
         else if (LAYOUT == kFixedStride)
             key_hashes_ptr<FLAVOR, true>(c, keys + i * key_len, key_len, h1, h2);
         else key_hashes_ptr<FLAVOR, false>(c, keys + b[p], (uint32_t)(e[p] - b[p]), h1, h2);
@@ -160,6 +199,9 @@ __device__ __forceinline__ void hashes_of(const FilterConsts &c, const uint8_t *
                                           uint64_t i, uint64_t *h1, uint64_t *h2) {
     if (LAYOUT == kFixed16) {
         key_hashes_16<FLAVOR>(c, keys, i, h1, h2);
+    } else if (LAYOUT == kFixed32) {
+        const ulonglong2 *kq = reinterpret_cast<const ulonglong2 *>(keys);
+        hash32<FLAVOR>(c, kq[2 * i], kq[2 * i + 1], h1, h2);
     } else if (LAYOUT == kFixedStride) {
         key_hashes_ptr<FLAVOR, true>(c, keys + i * key_len, key_len, h1, h2);
     } else {
@@ -569,7 +611,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
 #define NB_BIN_MIN_WAVES(NT) (2 * (NT) / 256)
 #endif
 template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY, int NT = kBinThreads,
-          bool STAGE = (LAYOUT != kFixed16), int KR = 0>
+          bool STAGE = !vec_layout(LAYOUT), int KR = 0>
 __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
     uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc, ENTRY *__restrict__ buckets) {
@@ -1511,7 +1553,7 @@ int launch_build_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         // and their in-tile ranks kept in registers while k <= 16 (NB_RANK=0: the
         // regenerate-and-recount variant, kept for A/B)
         const bool rank = env_u32("NB_RANK", 1) != 0;
-        if constexpr (LAYOUT == kFixed16) {
+        if constexpr (vec_layout(LAYOUT)) {
             if (c.k <= 8)
                 return rank ? launch_tiled<FLAVOR, LAYOUT, kBinKPT, kBinThreads, false, 8>(
                                   keys, offsets, key_len, n, c, words, overwrite, st)
@@ -1541,6 +1583,9 @@ int launch_build_f(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
                    const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st) {
     if (!offsets && key_len == 16 && (reinterpret_cast<uintptr_t>(keys) & 15) == 0)
         return launch_build_l<FLAVOR, kFixed16>(keys, offsets, key_len, n, c, words, overwrite, st);
+    if (!offsets && key_len == 32 && (reinterpret_cast<uintptr_t>(keys) & 15) == 0 &&
+        env_u32("NB_FIXED32", 1) != 0)
+        return launch_build_l<FLAVOR, kFixed32>(keys, offsets, key_len, n, c, words, overwrite, st);
     if (!offsets)
         return launch_build_l<FLAVOR, kFixedStride>(keys, offsets, key_len, n, c, words,
                                                     overwrite, st);
@@ -1554,6 +1599,9 @@ int launch_probe_f(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     const uint32_t *w32 = reinterpret_cast<const uint32_t *>(words);
     if (!offsets && key_len == 16 && (reinterpret_cast<uintptr_t>(keys) & 15) == 0)
         hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, kFixed16>), grid, block, 0, st, keys,
+                           offsets, key_len, n, c, w32, out);
+    else if (!offsets && key_len == 32 && (reinterpret_cast<uintptr_t>(keys) & 15) == 0)
+        hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, kFixed32>), grid, block, 0, st, keys,
                            offsets, key_len, n, c, w32, out);
     else if (!offsets)
         hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, kFixedStride>), grid, block, 0, st, keys,

@@ -213,6 +213,31 @@ def test_fixed_stride_layouts(dev, oracle, key_len, shift, build_path):
         np.testing.assert_array_equal(got, want)
 
 
+# D % 8 = 1, 0, 4, 5, 7, 3: every prefix class of the register-resident 32-byte path
+@pytest.mark.parametrize("seed", [7, 12345678, 12345678901234567890, 1234567890123,
+                                  123456789012345, 123])
+def test_fixed32_vector_path(dev, oracle, seed, build_path):
+    """32-byte keys at a 16-byte-aligned base (C5's shape) are hashed from two dwordx4
+    loads in registers (kFixed32); every seed-prefix class, both flavours, build and
+    probe, bit-exact; NB_FIXED32=0 keeps the LDS-staged path for the same keys."""
+    import os
+    from nasp_bloom import synth
+    n, m = 300_001, 4_000_037
+    buf = synth.fixed_keys(n, 32, seed=32)
+    for flavor in (0, 1):
+        want = oracle.build(flavor, buf, None, 32, n, m, 10, seed)
+        got = dev_build(dev, buf, None, 32, n, m, 10, seed, flavor=flavor)
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(oracle.probe(flavor, buf, None, 32, n, m, 10, seed, want),
+                                      dev_probe(dev, buf, None, 32, n, m, 10, seed, want, flavor))
+    os.environ["NB_FIXED32"] = "0"
+    try:
+        got = dev_build(dev, buf, None, 32, n, m, 10, seed)
+    finally:
+        del os.environ["NB_FIXED32"]
+    np.testing.assert_array_equal(got, oracle.build(0, buf, None, 32, n, m, 10, seed))
+
+
 @pytest.mark.parametrize("seed", [0, 7, 12345678, 123456789, 1234567890123456789, 2**64 - 1])
 def test_seed_prefix_lengths(dev, oracle, seed, build_path):
     """to_string(seed) of 1..20 digits changes how the prefix splices into h2."""
