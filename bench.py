@@ -286,6 +286,8 @@ def main():
                     help="skip the host-buffer (H2D + build + D2H) rate measurement")
     ap.add_argument("--no-probe", action="store_true", help="skip the batch-probe rates")
     ap.add_argument("--no-c2", action="store_true", help="skip the extra C2 line of the c4 run")
+    ap.add_argument("--no-rank-share", action="store_true",
+                    help="c5 at N=1: skip the per-rank (1B/8 keys) partial-build line")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
 
@@ -538,9 +540,40 @@ def bench_cooperative(args, wl, world, rank, dev):
            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                         "kernel": "whole cooperative step per GPU (build + merge collectives)"}}
+    if world == 1 and not args.no_rank_share:
+        res["per_rank_at_8"] = rank_share_rate(nbm, wl, keys, seed, args.flavor, dev, stream)
     if rank == 0:
         print(json.dumps(res), flush=True)
     dist.destroy_process_group()
+
+
+def rank_share_rate(nbm, wl, keys, seed, flavor, dev, stream, world=8, steps=3):
+    """What one rank of an 8-GPU C5 step builds: its 1/8 key range (125M x 32 B)
+    into the full-size partial filter (m = 2^32-1, k = 10, overwrite), device-resident
+    and timed on its own -- the merge collectives are not in this number."""
+    import torch
+    from nasp_bloom import distributed as D
+    b, e = D.shard_range(wl.n, 0, world)
+    n = e - b
+    words = torch.empty(nbm.nwords(wl.m), dtype=torch.int64, device=dev)
+
+    def step():
+        nbm.build_device(keys, None, wl.key_len, n, wl.m, wl.k, seed, flavor, words,
+                         stream=stream, overwrite=True)
+    step()
+    torch.cuda.synchronize(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    ms = ev0.elapsed_time(ev1) / steps
+    B = algorithmic_bytes(n, wl.key_len, n * wl.key_len, wl.m, False)
+    return {"keys": n, "ms": round(ms, 4), "value": round(n / (ms * 1e-3) / 1e6, 3),
+            "unit": "Mkeys/s", "frac": round(B / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+            "note": "one rank's share of an 8-GPU C5 step: 1B/8 keys into the full "
+                    "2^32-1-bit partial filter, one pass (merge collectives not included)"}
 
 
 if __name__ == "__main__":

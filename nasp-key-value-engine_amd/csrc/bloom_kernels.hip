@@ -667,15 +667,16 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     if (!STAGE) {
         KeyBatch<FLAVOR, LAYOUT, KPT> kb;
         kb.load(keys, offsets, base + tid, NT, n);
+        // every key of the lane hashed before any count atomic is issued: the
+        // compiler otherwise drains key p's LDS atomics (s_waitcnt lgkmcnt(0) at the
+        // join of the i < n branch) before it hashes key p + 1
+        uint64_t h1[KPT], h2[KPT];
 #pragma unroll
-        for (int p = 0; p < KPT; ++p) {
-            const uint64_t i = base + (uint64_t)p * NT + tid;
-            if (i < n) {
-                uint64_t h1, h2;
-                kb.hash(c, keys, key_len, i, p, &h1, &h2);
-                count_key(p, h1, h2);
-            }
-        }
+        for (int p = 0; p < KPT; ++p)  // (a lane past n hashes its stale registers)
+            kb.hash(c, keys, key_len, base + (uint64_t)p * NT + tid, p, &h1[p], &h2[p]);
+#pragma unroll
+        for (int p = 0; p < KPT; ++p)
+            if (base + (uint64_t)p * NT + tid < n) count_key(p, h1[p], h2[p]);
     } else {
         // Variable-length (or odd fixed-length) keys, one sub-batch of NT keys at a
         // time: its keys are one contiguous byte range.  When that fits the stage

@@ -79,7 +79,12 @@ def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len:
     the same (m, k, seed, flavor)."""
     world = dist.get_world_size(group)
     S = slice_words(m, world)
-    partial = torch.zeros(world * S, dtype=torch.int64, device=keys.device)
+    if build_fn is None:
+        # the device build overwrites the filter's words; only the slice padding needs zeros
+        partial = torch.empty(world * S, dtype=torch.int64, device=keys.device)
+        partial[nwords(m):].zero_()
+    else:  # a test-side builder may OR into the words
+        partial = torch.zeros(world * S, dtype=torch.int64, device=keys.device)
     if build_fn is None:
         build_device(keys, offsets, key_len, n, m, k, seed, flavor, partial, stream=stream,
                      overwrite=True)

@@ -41,7 +41,7 @@ def main():
                     env[k] = os.path.join(REPO, val) if k == "NB_LIB" else val
                 steps = min(args.steps, 3) if wl == "c5" else args.steps
                 cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--workload", wl,
-                       "--no-cpu-baseline", "--no-host-path", "--no-probe", "--no-c2",
+                       "--no-cpu-baseline", "--no-host-path", "--no-probe", "--no-c2", "--no-rank-share",
                        "--steps", str(steps), "--warmup", "1" if wl == "c5" else "3"]
                 r = subprocess.run(cmd, env=env, capture_output=True, text=True,
                                    timeout=args.timeout)
