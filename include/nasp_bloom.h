@@ -50,7 +50,13 @@ enum nb_status {
 /* Which std::hash<std::string> the reference binary was built with. */
 enum nb_flavor {
     NB_FLAVOR_LIBSTDCXX = 0,  /* GCC libstdc++ std::_Hash_bytes(p, len, 0xc70f6907) (Linux build) */
-    NB_FLAVOR_MSVC_FNV1A = 1  /* MSVC STL FNV-1a-64 (the authors' Windows build) */
+    NB_FLAVOR_MSVC_FNV1A = 1, /* MSVC STL FNV-1a-64 (the authors' Windows build) */
+    /* NOT the reference filter (no parity with any reference file): h1, h2 = the two
+     * halves of MurmurHash3_x64_128(key, len, (uint32_t)h2_seed) -- the reference's
+     * MurmurHash3/MurmurHash3.cpp:255-332 -- with the same (h1 + i*h2) % m closure.
+     * The north star's "k MurmurHash3_x64_128 hashes" wording; filter builds and
+     * probes only (nb_std_hash / Merkle stay std::hash flavours). */
+    NB_FLAVOR_MURMUR3_X64_128 = 2
 };
 
 /* ---------------------------------------------------------------- info --- */

@@ -33,6 +33,11 @@ uint64_t nb_std_hash(const uint8_t *p, uint64_t len, int flavor) {
         for (uint64_t b = 0; b < 8 && 8ull * j + b < len; ++b) w |= (uint64_t)p[8ull * j + b] << (8 * b);
         return w;
     };
+    if (flavor == NB_FLAVOR_MURMUR3_X64_128) {  // the first half, seed 0
+        uint64_t h1, h2;
+        nb::mm3_x64_128(load, (uint32_t)len, 0u, &h1, &h2);
+        return h1;
+    }
     return flavor == NB_FLAVOR_MSVC_FNV1A
                ? nb::hash1_aligned_words<NB_FLAVOR_MSVC_FNV1A>(load, 0, (uint32_t)len)
                : nb::hash1_aligned_words<NB_FLAVOR_LIBSTDCXX>(load, 0, (uint32_t)len);
@@ -100,7 +105,9 @@ void for_each_key_indices(const uint8_t *keys, const uint64_t *offsets, uint32_t
             return w;
         };
         uint64_t h1, h2;
-        if (flavor == NB_FLAVOR_MSVC_FNV1A)
+        if (flavor == NB_FLAVOR_MURMUR3_X64_128)
+            nb::hash_aligned_words<NB_FLAVOR_MURMUR3_X64_128>(c, load, a, len, &h1, &h2);
+        else if (flavor == NB_FLAVOR_MSVC_FNV1A)
             nb::hash_aligned_words<NB_FLAVOR_MSVC_FNV1A>(c, load, a, len, &h1, &h2);
         else if (offsets)
             nb::hash_aligned_words<NB_FLAVOR_LIBSTDCXX, decltype(load), false>(c, load, a, len, &h1, &h2);
@@ -113,7 +120,8 @@ void for_each_key_indices(const uint8_t *keys, const uint64_t *offsets, uint32_t
 }
 
 int cpu_args(uint64_t n, uint32_t m, uint32_t k, int flavor, const void *keys, const void *words) {
-    if (flavor != NB_FLAVOR_LIBSTDCXX && flavor != NB_FLAVOR_MSVC_FNV1A)
+    if (flavor != NB_FLAVOR_LIBSTDCXX && flavor != NB_FLAVOR_MSVC_FNV1A &&
+        flavor != NB_FLAVOR_MURMUR3_X64_128)
         return nb_internal_fail(NB_ERR_ARG, "unknown flavor");
     if (n && k && m == 0) return nb_internal_fail(NB_ERR_ARG, "m == 0 with keys (reference divides by zero)");
     if (n && k && (!keys || !words)) return nb_internal_fail(NB_ERR_ARG, "NULL keys or words");

@@ -90,7 +90,9 @@ __device__ __forceinline__ void lsx16(const FilterConsts &c, const ulonglong2 &k
 template <int FLAVOR>
 __device__ __forceinline__ void hash16(const FilterConsts &c, const ulonglong2 &kv, uint64_t *h1,
                                        uint64_t *h2) {
-    if (FLAVOR == NB_FLAVOR_MSVC_FNV1A) {
+    if (FLAVOR == NB_FLAVOR_MURMUR3_X64_128) {
+        nb::mm3_x64_128([&](uint32_t j) { return j ? kv.y : kv.x; }, 16, c.mm3_seed, h1, h2);
+    } else if (FLAVOR == NB_FLAVOR_MSVC_FNV1A) {
         uint64_t f1 = nb::kFnvBasis, f2 = c.fnv_pre;
         nb::fnv_consume(f1, f2, kv.x, 8);
         nb::fnv_consume(f1, f2, kv.y, 8);
@@ -146,7 +148,10 @@ template <int FLAVOR>
 __device__ __forceinline__ void hash32(const FilterConsts &c, const ulonglong2 &a,
                                        const ulonglong2 &b, uint64_t *h1, uint64_t *h2) {
     const uint64_t w[4] = {a.x, a.y, b.x, b.y};
-    if (FLAVOR == NB_FLAVOR_MSVC_FNV1A) {
+    if (FLAVOR == NB_FLAVOR_MURMUR3_X64_128) {
+        nb::mm3_x64_128([&](uint32_t j) { return j == 0 ? w[0] : j == 1 ? w[1] : j == 2 ? w[2] : w[3]; },
+                        32, c.mm3_seed, h1, h2);
+    } else if (FLAVOR == NB_FLAVOR_MSVC_FNV1A) {
         uint64_t f1 = nb::kFnvBasis, f2 = c.fnv_pre;
 #pragma unroll
         for (int j = 0; j < 4; ++j) nb::fnv_consume(f1, f2, w[j], 8);
@@ -1202,7 +1207,8 @@ uint32_t grid_for(uint64_t n) {
 }
 
 int check_common(uint64_t n, uint32_t m, int flavor, const void *keys, const void *words) {
-    if (flavor != NB_FLAVOR_LIBSTDCXX && flavor != NB_FLAVOR_MSVC_FNV1A)
+    if (flavor != NB_FLAVOR_LIBSTDCXX && flavor != NB_FLAVOR_MSVC_FNV1A &&
+        flavor != NB_FLAVOR_MURMUR3_X64_128)
         return fail(NB_ERR_ARG, "unknown flavor");
     if (n && m == 0) return fail(NB_ERR_ARG, "m == 0 with keys (reference divides by zero)");
     if (n && (!keys || !words)) return fail(NB_ERR_ARG, "NULL keys or words");
@@ -1627,6 +1633,9 @@ int launch_build(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
     if (!offsets) nb::set_fixed_len(c, key_len);
     if (env_u32("NB_FPMOD", 1) == 0) c.fm.fp = 0;  // A/B: integer remainders only
     g_device_builds.fetch_add(1, std::memory_order_relaxed);
+    if (flavor == NB_FLAVOR_MURMUR3_X64_128)
+        return launch_build_f<NB_FLAVOR_MURMUR3_X64_128>(keys, offsets, key_len, n, c, words,
+                                                         overwrite, st);
     return flavor == NB_FLAVOR_MSVC_FNV1A
                ? launch_build_f<NB_FLAVOR_MSVC_FNV1A>(keys, offsets, key_len, n, c, words,
                                                       overwrite, st)
@@ -1645,6 +1654,8 @@ int launch_probe(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
     FilterConsts c = nb::make_consts(m, k, seed, (uint32_t)flavor);
     if (!offsets) nb::set_fixed_len(c, key_len);
     if (env_u32("NB_FPMOD", 1) == 0) c.fm.fp = 0;
+    if (flavor == NB_FLAVOR_MURMUR3_X64_128)
+        return launch_probe_f<NB_FLAVOR_MURMUR3_X64_128>(keys, offsets, key_len, n, c, words, out, st);
     return flavor == NB_FLAVOR_MSVC_FNV1A
                ? launch_probe_f<NB_FLAVOR_MSVC_FNV1A>(keys, offsets, key_len, n, c, words, out, st)
                : launch_probe_f<NB_FLAVOR_LIBSTDCXX>(keys, offsets, key_len, n, c, words, out, st);

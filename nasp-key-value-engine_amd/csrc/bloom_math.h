@@ -53,6 +53,48 @@ NB_HD uint64_t lsx_init(uint64_t len) { return kStdSeed ^ (len * kMul); }
 
 NB_HD uint64_t fnv_step(uint64_t h, uint32_t byte) { return (h ^ byte) * kFnvPrime; }
 
+// MurmurHash3_x64_128 (the reference's MurmurHash3/MurmurHash3.cpp:255-332; used by
+// the non-parity NB_FLAVOR_MURMUR3_X64_128 only) over little-endian key words K(j),
+// zero beyond len: 16-byte blocks of two words, then the len & 15 tail.
+constexpr uint64_t kMmC1 = 0x87c37b91114253d5ULL, kMmC2 = 0x4cf5ad432745937fULL;
+NB_HD uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+NB_HD uint64_t fmix64(uint64_t k) {
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ULL;
+    return k ^ (k >> 33);
+}
+template <class LoadK>
+NB_HD void mm3_x64_128(LoadK K, uint32_t len, uint32_t seed, uint64_t *o1, uint64_t *o2) {
+    uint64_t h1 = seed, h2 = seed;
+    const uint32_t nb = len >> 4, rem = len & 15;
+    for (uint32_t i = 0; i < nb; ++i) {
+        const uint64_t k1 = rotl64(K(2 * i) * kMmC1, 31) * kMmC2;
+        h1 = (rotl64(h1 ^ k1, 27) + h2) * 5 + 0x52dce729;
+        const uint64_t k2 = rotl64(K(2 * i + 1) * kMmC2, 33) * kMmC1;
+        h2 = (rotl64(h2 ^ k2, 31) + h1) * 5 + 0x38495ab5;
+    }
+    if (rem > 8) {  // (the reference's switch falls through: k2 first, then k1)
+        const uint64_t t = K(2 * nb + 1) & ((1ull << (8 * (rem - 8))) - 1);
+        h2 ^= rotl64(t * kMmC2, 33) * kMmC1;
+    }
+    if (rem) {
+        const uint64_t t = rem >= 8 ? K(2 * nb) : K(2 * nb) & ((1ull << (8 * rem)) - 1);
+        h1 ^= rotl64(t * kMmC1, 31) * kMmC2;
+    }
+    h1 ^= len;
+    h2 ^= len;
+    h1 += h2;
+    h2 += h1;
+    h1 = fmix64(h1);
+    h2 = fmix64(h2);
+    h1 += h2;
+    h2 += h1;
+    *o1 = h1;
+    *o2 = h2;
+}
+
 // ------------------------------------------------------------- fast mod ----
 struct FastMod {
     uint32_t m;   // divisor (>= 1)
@@ -159,6 +201,7 @@ struct FilterConsts {
     uint64_t h2_init_fixed; // libstdc++ h2 state after the whole prefix words, for
                             // keys of length fixed_len (fixed-length layouts only)
     uint32_t fixed_len;
+    uint32_t mm3_seed;      // NB_FLAVOR_MURMUR3_X64_128: (uint32_t)h2_seed
 };
 
 inline FilterConsts make_consts(uint32_t m, uint32_t k, uint64_t seed, uint32_t flavor) {
@@ -191,6 +234,7 @@ inline FilterConsts make_consts(uint32_t m, uint32_t k, uint64_t seed, uint32_t 
     c.fnv_pre = h;
     c.fixed_len = 0;
     c.h2_init_fixed = 0;
+    c.mm3_seed = (uint32_t)seed;
     return c;
 }
 
@@ -310,6 +354,14 @@ NB_HD void hash_aligned_words(const FilterConsts &c, LoadQ Q, uint32_t a, uint32
                               uint64_t *h1, uint64_t *h2) {
     const uint32_t nq = (a + len + 7) >> 3;
     const uint32_t nk = (len + 7) >> 3;
+    if (FLAVOR == 2) {  // MurmurHash3_x64_128 (non-parity flavour)
+        auto K = [&](uint32_t j) {
+            const uint64_t lo = j < nq ? Q(j) : 0, hi = j + 1 < nq ? Q(j + 1) : 0;
+            return mask_bytes(funnel(lo, hi, 8 * a), (int)(len - 8 * j));
+        };
+        mm3_x64_128(K, len, c.mm3_seed, h1, h2);
+        return;
+    }
     uint64_t qcur = nq ? Q(0) : 0;
     if (FLAVOR == 1) {
         uint64_t f1 = kFnvBasis, f2 = c.fnv_pre;
@@ -515,6 +567,15 @@ inline void key_hashes_host(const FilterConsts &c, const uint8_t *p, uint64_t le
         for (uint64_t b = 0; b < nb; ++b) r |= (uint64_t)q[b] << (8 * b);
         return r;
     };
+    if (c.flavor == 2) {
+        auto K = [&](uint32_t j) {
+            uint64_t w = 0;
+            for (uint64_t b = 0; b < 8 && 8ull * j + b < len; ++b) w |= (uint64_t)p[8ull * j + b] << (8 * b);
+            return w;
+        };
+        mm3_x64_128(K, (uint32_t)len, c.mm3_seed, h1o, h2o);
+        return;
+    }
     if (c.flavor == 1) {
         uint64_t a = kFnvBasis, b = c.fnv_pre;
         for (uint64_t i = 0; i < len; ++i) { a = fnv_step(a, p[i]); b = fnv_step(b, p[i]); }

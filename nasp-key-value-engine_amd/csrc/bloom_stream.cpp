@@ -167,7 +167,8 @@ int nb_builder_create(uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
                       const uint64_t *init_words, int device, nb_builder **out) {
     if (!out) return nb_internal_fail(NB_ERR_ARG, "NULL out");
     *out = nullptr;
-    if (flavor != NB_FLAVOR_LIBSTDCXX && flavor != NB_FLAVOR_MSVC_FNV1A)
+    if (flavor != NB_FLAVOR_LIBSTDCXX && flavor != NB_FLAVOR_MSVC_FNV1A &&
+        flavor != NB_FLAVOR_MURMUR3_X64_128)
         return nb_internal_fail(NB_ERR_ARG, "unknown flavor");
     int count = 0;
     if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
@@ -437,7 +438,8 @@ int merge_slice(std::vector<nb_builder *> &bs, int o, uint64_t lo, uint64_t len,
 extern "C" int nb_build_sharded(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
                                 uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
                                 uint64_t *words, int nshards) {
-    if (flavor != NB_FLAVOR_LIBSTDCXX && flavor != NB_FLAVOR_MSVC_FNV1A)
+    if (flavor != NB_FLAVOR_LIBSTDCXX && flavor != NB_FLAVOR_MSVC_FNV1A &&
+        flavor != NB_FLAVOR_MURMUR3_X64_128)
         return nb_internal_fail(NB_ERR_ARG, "unknown flavor");
     if (n && m == 0) return nb_internal_fail(NB_ERR_ARG, "m == 0 with keys (reference divides by zero)");
     if (n && (!keys || !words)) return nb_internal_fail(NB_ERR_ARG, "NULL keys or words");

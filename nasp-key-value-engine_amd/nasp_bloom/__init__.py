@@ -14,7 +14,8 @@ is the Python binding used by tests/ and bench.py:
                                   of the reference class (MerkleTree/MerkleTree.h:10-36)
   distributed                  -- multi-GPU: independent filters / cooperative OR-merge
 """
-from ._lib import (FLAVOR_LIBSTDCXX, FLAVOR_MSVC_FNV1A, NaspBloomError, lib)  # noqa: F401
+from ._lib import (FLAVOR_LIBSTDCXX, FLAVOR_MSVC_FNV1A, FLAVOR_MURMUR3_X64_128,  # noqa: F401
+                   NaspBloomError, lib)
 from .api import (BloomFilter, Builder, MerkleTree, build_device, merkle_device, merkle_host,  # noqa: F401
                   merkle_tree_size, std_hash, build_host, build_host_sharded, deserialize, nwords, or_merge_device,  # noqa: F401
                   probe_device, probe_host, build_cpu, probe_cpu, device_build_count, seed_from_time, serialize, size_of_bitset,

@@ -22,6 +22,7 @@ BUILD_OVERWRITE = 1
 
 FLAVOR_LIBSTDCXX = 0
 FLAVOR_MSVC_FNV1A = 1
+FLAVOR_MURMUR3_X64_128 = 2  # non-parity (include/nasp_bloom.h)
 
 # every symbol include/nasp_bloom.h declares: (restype, argtypes)
 _u8p = C.c_void_p

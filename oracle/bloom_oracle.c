@@ -58,7 +58,50 @@ uint64_t orc_hash_fnv1a(const uint8_t *p, size_t len) {
     return h;
 }
 
+/* MurmurHash3_x64_128, by behaviour (reference MurmurHash3/MurmurHash3.cpp:255-332):
+ * 16-byte blocks as two little-endian 64-bit lanes, the len & 15 tail (the high
+ * lane first, as the reference's fall-through switch does), then fmix64. */
+#define MM_C1 0x87c37b91114253d5ULL
+#define MM_C2 0x4cf5ad432745937fULL
+static inline uint64_t rotl(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+static inline uint64_t fmix(uint64_t k) {
+    k ^= k >> 33; k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ULL;
+    return k ^ (k >> 33);
+}
+void orc_murmur3_x64_128(const uint8_t *p, size_t len, uint32_t seed, uint64_t out[2]) {
+    uint64_t h1 = seed, h2 = seed;
+    const size_t nb = len / 16;
+    for (size_t i = 0; i < nb; ++i) {
+        uint64_t k1 = load_le(p + 16 * i, 8), k2 = load_le(p + 16 * i + 8, 8);
+        k1 *= MM_C1; k1 = rotl(k1, 31); k1 *= MM_C2; h1 ^= k1;
+        h1 = rotl(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+        k2 *= MM_C2; k2 = rotl(k2, 33); k2 *= MM_C1; h2 ^= k2;
+        h2 = rotl(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+    }
+    const uint8_t *t = p + 16 * nb;
+    const size_t rem = len & 15;
+    if (rem > 8) {
+        uint64_t k2 = load_le(t + 8, rem - 8);
+        k2 *= MM_C2; k2 = rotl(k2, 33); k2 *= MM_C1; h2 ^= k2;
+    }
+    if (rem) {
+        uint64_t k1 = load_le(t, rem < 8 ? rem : 8);
+        k1 *= MM_C1; k1 = rotl(k1, 31); k1 *= MM_C2; h1 ^= k1;
+    }
+    h1 ^= (uint64_t)len; h2 ^= (uint64_t)len;
+    h1 += h2; h2 += h1;
+    h1 = fmix(h1); h2 = fmix(h2);
+    h1 += h2; h2 += h1;
+    out[0] = h1; out[1] = h2;
+}
+
 uint64_t orc_hash(int flavor, const uint8_t *p, size_t len) {
+    if (flavor == ORC_FLAVOR_MURMUR3_X64_128) {  /* first half, seed 0 */
+        uint64_t o[2];
+        orc_murmur3_x64_128(p, len, 0, o);
+        return o[0];
+    }
     return flavor == ORC_FLAVOR_MSVC_FNV1A ? orc_hash_fnv1a(p, len)
                                             : orc_hash_libstdcxx(p, len);
 }
@@ -136,10 +179,18 @@ typedef struct {
     uint32_t m;
     char digits[24];
     int ndig;
+    uint64_t seed;
 } orc_ctx;
 
 static void key_hashes(const orc_ctx *c, const uint8_t *key, size_t len,
                        uint64_t *h1, uint64_t *h2, uint8_t *scratch) {
+    if (c->flavor == ORC_FLAVOR_MURMUR3_X64_128) {  /* not the reference filter */
+        uint64_t o[2];
+        orc_murmur3_x64_128(key, len, (uint32_t)c->seed, o);
+        *h1 = o[0];
+        *h2 = o[1];
+        return;
+    }
     *h1 = orc_hash(c->flavor, key, len);
     *h2 = hash_with_prefix(c->flavor, c->digits, c->ndig, key, len, scratch);
 }
@@ -151,7 +202,7 @@ static inline uint32_t index_of(uint64_t h1, uint64_t h2, uint32_t i, uint32_t m
 
 uint32_t orc_index(int flavor, const uint8_t *key, size_t len, uint32_t i,
                    uint32_t m, uint64_t seed) {
-    orc_ctx c = {flavor, m, {0}, 0};
+    orc_ctx c = {flavor, m, {0}, 0, seed};
     c.ndig = orc_seed_digits(seed, c.digits);
     uint8_t stackbuf[512];
     uint8_t *scratch = len + 24 <= sizeof stackbuf ? stackbuf : (uint8_t *)malloc(len + 24);
@@ -176,7 +227,7 @@ int orc_build(int flavor, const uint8_t *keys, const uint64_t *offsets,
               uint64_t seed, uint64_t *words) {
     if (n == 0) return 0;
     if (m == 0) return -1; /* the reference divides by zero here */
-    orc_ctx c = {flavor, m, {0}, 0};
+    orc_ctx c = {flavor, m, {0}, 0, seed};
     c.ndig = orc_seed_digits(seed, c.digits);
     uint8_t *scratch = (uint8_t *)malloc(max_key_len(offsets, key_len, n) + 24);
     for (uint64_t i = 0; i < n; ++i) {
@@ -198,7 +249,7 @@ int orc_probe(int flavor, const uint8_t *keys, const uint64_t *offsets,
               uint64_t seed, const uint64_t *words, uint8_t *out) {
     if (n == 0) return 0;
     if (m == 0 && k > 0) return -1;
-    orc_ctx c = {flavor, m, {0}, 0};
+    orc_ctx c = {flavor, m, {0}, 0, seed};
     c.ndig = orc_seed_digits(seed, c.digits);
     uint8_t *scratch = (uint8_t *)malloc(max_key_len(offsets, key_len, n) + 24);
     for (uint64_t i = 0; i < n; ++i) {

@@ -19,7 +19,11 @@
 extern "C" {
 #endif
 
-enum { ORC_FLAVOR_LIBSTDCXX = 0, ORC_FLAVOR_MSVC_FNV1A = 1 };
+enum { ORC_FLAVOR_LIBSTDCXX = 0, ORC_FLAVOR_MSVC_FNV1A = 1,
+       /* non-parity: (h1, h2) = MurmurHash3_x64_128(key, len, (uint32_t)seed) */
+       ORC_FLAVOR_MURMUR3_X64_128 = 2 };
+/* MurmurHash3_x64_128 restated (reference MurmurHash3/MurmurHash3.cpp:255-332). */
+void orc_murmur3_x64_128(const uint8_t *p, size_t len, uint32_t seed, uint64_t out[2]);
 
 /* std::hash<std::string> of each platform (reference BloomFilter.cpp:59-60). */
 uint64_t orc_hash_libstdcxx(const uint8_t *p, size_t len);

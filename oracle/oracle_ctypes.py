@@ -66,6 +66,8 @@ class Oracle:
         lib.orc_num_hashes.argtypes = [C.c_uint32, C.c_uint32]
         lib.orc_seed_from_time.restype = C.c_uint64
         lib.orc_seed_from_time.argtypes = [C.c_uint32]
+        lib.orc_murmur3_x64_128.restype = None
+        lib.orc_murmur3_x64_128.argtypes = [_u8p, C.c_size_t, C.c_uint32, _u64p]
         lib.orc_index.restype = C.c_uint32
         lib.orc_index.argtypes = [C.c_int, _u8p, C.c_size_t, C.c_uint32, C.c_uint32, C.c_uint64]
         lib.orc_build.restype = C.c_int
@@ -131,6 +133,26 @@ class Oracle:
         root = self.lib.orc_merkle(flavor, _ptr(data_u8), _ptr(offsets, _u64p), rec_len, n,
                                    _ptr(leaves, _u64p), _ptr(tree, _u64p))
         return int(root), leaves[:n], tree
+
+
+def murmur3_x64_128(lib, data: bytes, seed: int, fn: str = "orc_murmur3_x64_128"):
+    """(h1, h2) of MurmurHash3_x64_128 through the oracle (default) or the reference
+    shim (lib = RefMurmur3().lib, fn = "ref_murmur3_x64_128")."""
+    buf = np.frombuffer(data, dtype=np.uint8).copy() if data else np.zeros(1, np.uint8)
+    out = np.zeros(2, dtype=np.uint64)
+    getattr(lib, fn)(_ptr(buf), len(data), seed, _ptr(out, _u64p))
+    return int(out[0]), int(out[1])
+
+
+class RefMurmur3:
+    """The reference MurmurHash3.cpp compiled here (oracle/_ref/libref_murmur3.so)."""
+
+    def __init__(self, path: str = os.path.join(os.path.dirname(REF_SO), "libref_murmur3.so")):
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        self.lib = C.CDLL(path)
+        self.lib.ref_murmur3_x64_128.restype = None
+        self.lib.ref_murmur3_x64_128.argtypes = [_u8p, C.c_int, C.c_uint32, _u64p]
 
 
 class RefLib:

@@ -213,6 +213,27 @@ def test_fixed_stride_layouts(dev, oracle, key_len, shift, build_path):
         np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("layout", ["fixed16", "fixed32", "stride7", "varlen"])
+def test_murmur3_flavor_device(dev, oracle, layout, build_path):
+    """The optional non-parity NB_FLAVOR_MURMUR3_X64_128 (h1, h2 = the halves of
+    MurmurHash3_x64_128(key, len, (uint32_t)seed)) on the device against the
+    oracle (itself pinned to the compiled reference MurmurHash3.cpp), every key
+    layout path, build and probe."""
+    from nasp_bloom import synth
+    n, m, k = 200_003, 4_000_037, 7
+    if layout == "varlen":
+        buf, offs = synth.var_keys(n, 0, 70)
+        kl = 0
+    else:
+        kl = {"fixed16": 16, "fixed32": 32, "stride7": 7}[layout]
+        buf, offs = synth.fixed_keys(n, kl), None
+    want = oracle.build(2, buf, offs, kl, n, m, k, SEED)
+    got = dev_build(dev, buf, offs, kl, n, m, k, SEED, flavor=2)
+    np.testing.assert_array_equal(got, want)
+    np.testing.assert_array_equal(dev_probe(dev, buf, offs, kl, n, m, k, SEED, want, 2),
+                                  oracle.probe(2, buf, offs, kl, n, m, k, SEED, want))
+
+
 # D % 8 = 1, 0, 4, 5, 7, 3: every prefix class of the register-resident 32-byte path
 @pytest.mark.parametrize("seed", [7, 12345678, 12345678901234567890, 1234567890123,
                                   123456789012345, 123])
