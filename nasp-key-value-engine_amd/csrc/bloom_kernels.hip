@@ -294,7 +294,10 @@ constexpr int kShards = 8;
 constexpr uint32_t kStageBytes = 48 * 1024;  // LDS staging window for variable-length keys
 constexpr uint32_t kLenClasses = 16;         // word-count classes of the staged keys' order
 // the stage is followed by the length permutation: key info [NT] | order [NT] | classes
-constexpr size_t stage_lds_bytes(int nt) { return kStageBytes + (2 * (size_t)nt + kLenClasses) * 4; }
+constexpr uint32_t kInitLens = 72;           // per-length hash start states tabulated (0..71 B)
+constexpr size_t stage_lds_bytes(int nt) {
+    return kStageBytes + (2 * (size_t)nt + kLenClasses) * 4 + 2 * kInitLens * 8;
+}
 constexpr uint32_t kMaxTiles = 4096;
 
 // Diagnostic builds (tools/ubench_tiled.hip) stop a kernel after a phase to price
@@ -692,6 +695,16 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
         auto koff = [&](uint64_t i) -> uint64_t {
             return LAYOUT == kOffsets ? offsets[i] : i * (uint64_t)key_len;
         };
+        // libstdc++ start states per key length (h1: lsx_init, h2: after the seed's
+        // whole prefix words), tabulated once per block after the stage's key-info,
+        // permutation and class arrays; the first sub-batch's barrier publishes them
+        uint64_t *init_tab = reinterpret_cast<uint64_t *>(
+            stage + kStageBytes + (2 * (size_t)NT + kLenClasses) * 4);  // [2][kInitLens]
+        if (FLAVOR == NB_FLAVOR_LIBSTDCXX && tid < kInitLens) {
+            init_tab[tid] = nb::lsx_init(tid);
+            init_tab[kInitLens + tid] =
+                LAYOUT == kFixedStride ? c.h2_init_fixed : nb::lsx_h2_start(c, tid);
+        }
 #pragma unroll
         for (int p = 0; p < KPT; ++p) {
             const uint64_t pb = base + (uint64_t)p * NT;  // first key of the sub-batch
@@ -760,11 +773,17 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
                     const uint32_t *dw = reinterpret_cast<const uint32_t *>(stage) + (klo >> 2);
                     auto D = [dw](uint32_t j) { return dw[j]; };
                     const uint32_t sh = 8 * (klo & 3u);
-                    const uint64_t g0 =
-                        LAYOUT == kFixedStride ? c.h2_init_fixed : nb::lsx_h2_start(c, len);
-                    if (c.prem == 0) nb::lsx_hash_dwords<0>(c, D, sh, len, g0, &h1, &h2);
-                    else if (c.prem <= 4) nb::lsx_hash_dwords<1>(c, D, sh, len, g0, &h1, &h2);
-                    else nb::lsx_hash_dwords<2>(c, D, sh, len, g0, &h1, &h2);
+                    uint64_t h0, g0;
+                    if (len < kInitLens) {
+                        h0 = init_tab[len];
+                        g0 = init_tab[kInitLens + len];
+                    } else {
+                        h0 = nb::lsx_init(len);
+                        g0 = LAYOUT == kFixedStride ? c.h2_init_fixed : nb::lsx_h2_start(c, len);
+                    }
+                    if (c.prem == 0) nb::lsx_hash_dwords<0>(c, D, sh, len, h0, g0, &h1, &h2);
+                    else if (c.prem <= 4) nb::lsx_hash_dwords<1>(c, D, sh, len, h0, g0, &h1, &h2);
+                    else nb::lsx_hash_dwords<2>(c, D, sh, len, h0, g0, &h1, &h2);
                 } else if (staged) {
                     const uint32_t lo = klo, a = lo & 7u;
                     const uint64_t *q = reinterpret_cast<const uint64_t *>(stage + (lo - a));

@@ -417,14 +417,15 @@ NB_HD uint64_t lsx_splice(uint64_t kwp, uint64_t kw, uint32_t p) {
 
 // h1 = H(key), h2 = H(to_string(seed) ++ key) for a key of len bytes starting at
 // bit sh (0, 8, 16, 24) of dword D(0); D(i) returns dword i, and reads run up to
-// 12 bytes past the key's last byte.  g0: h2's state after the whole prefix words
-// (lsx_init(len + D) mixed with pre_d, or c.h2_init_fixed for fixed-length keys).
+// 12 bytes past the key's last byte.  h0 = lsx_init(len); g0: h2's state after the
+// whole prefix words (lsx_h2_start(c, len), or c.h2_init_fixed for fixed-length
+// keys) -- both per length, so a kernel may take them from a table.
 template <int PC, class LoadD>
-NB_HD void lsx_hash_dwords(const FilterConsts &c, LoadD D, uint32_t sh, uint32_t len, uint64_t g0,
-                           uint64_t *h1o, uint64_t *h2o) {
+NB_HD void lsx_hash_dwords(const FilterConsts &c, LoadD D, uint32_t sh, uint32_t len, uint64_t h0,
+                           uint64_t g0, uint64_t *h1o, uint64_t *h2o) {
     const uint32_t L8 = len >> 3, rem = len & 7, p = c.prem;
     auto mask = [](uint64_t x, uint32_t nb) { return x & ((1ull << (8 * nb)) - 1); };
-    uint64_t h = lsx_init(len), g = g0;
+    uint64_t h = h0, g = g0;
     uint64_t kwp = PC ? c.pre_tail << (64 - 8 * p) : 0;  // key word -1 as the splice sees it
     uint32_t d0 = D(0), d1 = D(1);
     for (uint32_t j = 0; j < L8; ++j) {  // whole key words and whole stream words

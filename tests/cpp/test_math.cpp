@@ -106,9 +106,9 @@ int main() {
                     const uint32_t pc = c.prem == 0 ? 0 : c.prem <= 4 ? 1 : 2;
                     for (int fixed = 0; fixed < 2; ++fixed) {
                         const uint64_t g0 = fixed ? cf.h2_init_fixed : nb::lsx_h2_start(c, (uint32_t)len);
-                        if (pc == 0) nb::lsx_hash_dwords<0>(c, D, 8 * b, (uint32_t)len, g0, &g1, &g2);
-                        else if (pc == 1) nb::lsx_hash_dwords<1>(c, D, 8 * b, (uint32_t)len, g0, &g1, &g2);
-                        else nb::lsx_hash_dwords<2>(c, D, 8 * b, (uint32_t)len, g0, &g1, &g2);
+                        if (pc == 0) nb::lsx_hash_dwords<0>(c, D, 8 * b, (uint32_t)len, nb::lsx_init(len), g0, &g1, &g2);
+                        else if (pc == 1) nb::lsx_hash_dwords<1>(c, D, 8 * b, (uint32_t)len, nb::lsx_init(len), g0, &g1, &g2);
+                        else nb::lsx_hash_dwords<2>(c, D, 8 * b, (uint32_t)len, nb::lsx_init(len), g0, &g1, &g2);
                         if (g1 != h1 || g2 != h2) ++hbad;
                     }
                 }
