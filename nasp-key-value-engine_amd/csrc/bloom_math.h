@@ -442,13 +442,13 @@ NB_HD void lsx_hash_dwords(const FilterConsts &c, LoadD D, uint32_t sh, uint32_t
     if (rem) h = lsx_tail(h, mask(kwt, rem));
     // stream word L8 holds p + rem valid bytes: a whole round when that reaches 8,
     // then word L8 + 1 holds the rest (p + rem - 8, from kwt alone)
+    // (one straight-line step with selects: its lanes' p + rem differ, and
+    // divergent branches would run every case for the whole wave)
     const uint32_t sv = p + rem;
-    if (sv >= 8) {
-        g = lsx_round(g, lsx_splice<PC>(kwp, kwt, p));
-        if (sv > 8) g = lsx_tail(g, mask(lsx_splice<PC>(kwt, 0, p), sv - 8));
-    } else if (sv) {
-        g = lsx_tail(g, mask(lsx_splice<PC>(kwp, kwt, p), sv));
-    }
+    const uint64_t s8 = lsx_splice<PC>(kwp, kwt, p);
+    const uint64_t x = sv >= 8 ? shift_mix(s8 * kMul) * kMul : mask(s8, sv);
+    if (sv) g = (g ^ x) * kMul;  // a whole round (sv >= 8) or the tail
+    if (sv > 8) g = lsx_tail(g, mask(lsx_splice<PC>(kwt, 0, p), sv - 8));
     *h1o = lsx_final(h);
     *h2o = lsx_final(g);
 }
