@@ -286,6 +286,18 @@ struct TileCfg {
                      // fine tiles' ts
 };
 
+// Bucket unit of pass 1 of the two-level build: five 25-bit in-super-tile offsets
+// per 16 bytes (3.2 B per entry instead of a 32-bit index).
+struct alignas(16) Pack5 {
+    uint32_t x, y, z, w;
+};
+// entries per bucket unit of an entry type: u64 = three 21-bit offsets, Pack5 = five
+// 25-bit ones, else one
+template <typename ENTRY>
+__host__ __device__ constexpr uint32_t pack_of() {
+    return sizeof(ENTRY) == 16 ? 5u : sizeof(ENTRY) == 8 ? 3u : 1u;
+}
+
 constexpr int kBinThreads = 1024;
 constexpr int kBinKPT = 2;       // keys per thread when k <= 8 (1 for larger k)
 constexpr int kTileThreads = 1024;
@@ -420,10 +432,12 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     uint32_t *wave_sums = lds + 2 * T;    // [kWaves + 1]
     const uint32_t lds0 = lds_addr(lds);
     const uint32_t sort_b = lds0 + sort_off_words * 4;  // absolute LDS byte address
-    // packed entries (ENTRY = u64, 3 in-tile offsets per word): every run takes a
-    // whole number of words, its 1-2 pad slots hold copies of its first entry
-    constexpr bool PACK = sizeof(ENTRY) == 8;
-    auto slots = [](uint32_t c) { return PACK ? (c + 2) / 3 * 3 : c; };
+    // packed entries (ENTRY = u64, 3 in-tile offsets per word; Pack5, 5 per 16
+    // bytes): every run takes a whole number of units, its 1..PK-1 pad slots hold
+    // copies of its first entry
+    constexpr uint32_t PK = pack_of<ENTRY>();
+    constexpr bool PACK = PK > 1;
+    auto slots = [](uint32_t c) { return PACK ? (c + PK - 1) / PK * PK : c; };
     auto count_of = [&](uint32_t t) { return (cnt[t] - ((lds0 + 4 * t) << 16)) >> 2; };
     // ---- phase 2: scan (one round), reservations
     const uint32_t t0 = 2 * tid;
@@ -454,7 +468,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     }
     const uint32_t shard = blockIdx.x & (tc.G - 1);  // G is a power of two
     uint32_t *cur = sc.gcur + (size_t)shard * T;
-    const uint32_t ua = PACK ? (ha + 2) / 3 : ha, ub = PACK ? (hb + 2) / 3 : hb;  // bucket units
+    const uint32_t ua = (ha + PK - 1) / PK, ub = (hb + PK - 1) / PK;  // bucket units
     uint32_t ga = 0, gb = 0;
     if (wid * 64 < T) {  // wave-uniform
         if (ua) ga = atomicAdd(&cur[ta], ua);
@@ -488,19 +502,22 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     // overflow.  (packed: st and the table in words; the pad slots are filled here
     // -- the placement is complete, and nothing else touches the sort area until
     // phase 4)
-    const bool b32 = (uint64_t)T * tc.G * tc.cap * sizeof(ENTRY) <= 0xFFFFFFFFull;
+    // (Pack5 units are always addressed by unit index: esz 1)
+    const bool b32 = PK < 5 && (uint64_t)T * tc.G * tc.cap * sizeof(ENTRY) <= 0xFFFFFFFFull;
     const uint32_t esz = (b32 && !any_ovf) ? (uint32_t)sizeof(ENTRY) : 1u;
     auto run_entry = [&](uint32_t t, uint32_t g, uint32_t h) {
         uint32_t st = (cnt[t] - sort_b) / 4;
-        if (PACK) {  // 0-2 pad slots (straight-line: the compiler would emit a memset loop)
+        if (PACK) {  // 0..PK-1 pad slots (straight-line: the compiler would emit a memset loop)
             uint32_t *run = lds + sort_off_words + st;
             const uint32_t np = slots(h) - h;
             if (np) {
                 const uint32_t v0 = run[0];
                 run[h] = v0;
                 if (np > 1) run[h + 1] = v0;
+                if (PK > 3 && np > 2) run[h + 2] = v0;
+                if (PK > 3 && np > 3) run[h + 3] = v0;
             }
-            st /= 3;
+            st /= PK;
         }
         GX[t] = ((t * tc.G + shard) * tc.cap + g - st) * esz;
         return st;
@@ -518,7 +535,34 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     // ---- phase 4: coalesced write-out, four independent entries per lane per step
     const uint32_t *sorted = lds + sort_off_words;
     const uint32_t *S4 = cnt;  // limits (overflow only)
-    if constexpr (PACK) {
+    if constexpr (PK == 5) {
+        // unit q of the block = slots 5q..5q+4 (one run, super tile of the first
+        // slot): 25-bit fields at bits 0, 25, 50, 75, 100 of the 16 bytes
+        const uint32_t units = total / 5, msk = (1u << tc.ts) - 1;
+        Pack5 *bu = reinterpret_cast<Pack5 *>(buckets);
+        for (uint32_t q = tid; q < units; q += NT) {
+            const uint32_t *s5 = sorted + 5 * q;  // stride 5: conflict-free
+            const uint32_t a = s5[0], t = a >> tc.ts;
+            if (!any_ovf || q < S4[t]) {
+                const uint32_t f0 = a & msk, f1 = s5[1] & msk, f2 = s5[2] & msk,
+                               f3 = s5[3] & msk, f4 = s5[4] & msk;
+                Pack5 u;
+                u.x = f0 | (f1 << 25);
+                u.y = (f1 >> 7) | (f2 << 18);
+                u.z = (f2 >> 14) | (f3 << 11);
+                u.w = (f3 >> 21) | (f4 << 4);
+                bu[(uint32_t)(GX[t] + q)] = u;
+            } else {  // past the bucket's capacity: the five entries to the spill bitmap
+                for (uint32_t r = 0; r < 5; ++r) {
+                    const uint32_t v = s5[r];
+                    __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    sc.spill_flag[v >> tc.fts] = 1u;
+                }
+            }
+        }
+        return;
+    } else if constexpr (PACK) {
         // word q of the block = slots 3q..3q+2 (one run, tile of the first slot)
         const uint32_t words = total / 3, msk = (1u << tc.ts) - 1;
         auto word_at = [&](uint32_t q, uint32_t *t) {
@@ -561,54 +605,55 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
             }
         }
         return;
-    }
-    if (!any_ovf && b32) {
-        char *bb = reinterpret_cast<char *>(buckets);
-        uint32_t j = tid;
-        for (; j + 3 * NT < total; j += 4 * NT) {
-            uint32_t v[4], g[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) g[u] = NB_DIAG_WO == 2 ? 0u : GX[v[u] >> tc.ts];
-            if (NB_DIAG_WO == 1) {  // diagnostic: LDS reads only
-                if ((v[0] ^ v[1] ^ v[2] ^ v[3] ^ g[0] ^ g[1] ^ g[2] ^ g[3]) == 0xFFFFFFFFu) bb[0] = 1;
-                continue;
-            }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                *reinterpret_cast<ENTRY *>(bb + (g[u] + (j + u * NT) * (uint32_t)sizeof(ENTRY))) =
-                    (ENTRY)v[u];
-        }
-        for (; j < total; j += NT) {
-            const uint32_t v = sorted[j];
-            *reinterpret_cast<ENTRY *>(bb + (GX[v >> tc.ts] + j * (uint32_t)sizeof(ENTRY))) = (ENTRY)v;
-        }
-    } else if (!any_ovf) {  // buckets past 4 GiB: entry indices, 64-bit addresses
-        uint32_t j = tid;
-        for (; j + 3 * NT < total; j += 4 * NT) {
-            uint32_t v[4], g[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) g[u] = GX[v[u] >> tc.ts];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) buckets[(uint32_t)(g[u] + j + u * NT)] = (ENTRY)v[u];
-        }
-        for (; j < total; j += NT) {
-            const uint32_t v = sorted[j];
-            buckets[(uint32_t)(GX[v >> tc.ts] + j)] = (ENTRY)v;
-        }
     } else {
-        // overflow: entries past a bucket's capacity go to the spill bitmap
-        for (uint32_t j = tid; j < total; j += NT) {
-            const uint32_t v = sorted[j], t = v >> tc.ts;
-            if (j < S4[t]) {
-                buckets[(uint32_t)(GX[t] + j)] = (ENTRY)v;
-            } else {
-                __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-                sc.spill_flag[v >> tc.fts] = 1u;
+        if (!any_ovf && b32) {
+            char *bb = reinterpret_cast<char *>(buckets);
+            uint32_t j = tid;
+            for (; j + 3 * NT < total; j += 4 * NT) {
+                uint32_t v[4], g[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) g[u] = NB_DIAG_WO == 2 ? 0u : GX[v[u] >> tc.ts];
+                if (NB_DIAG_WO == 1) {  // diagnostic: LDS reads only
+                    if ((v[0] ^ v[1] ^ v[2] ^ v[3] ^ g[0] ^ g[1] ^ g[2] ^ g[3]) == 0xFFFFFFFFu) bb[0] = 1;
+                    continue;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    *reinterpret_cast<ENTRY *>(bb + (g[u] + (j + u * NT) * (uint32_t)sizeof(ENTRY))) =
+                        (ENTRY)v[u];
+            }
+            for (; j < total; j += NT) {
+                const uint32_t v = sorted[j];
+                *reinterpret_cast<ENTRY *>(bb + (GX[v >> tc.ts] + j * (uint32_t)sizeof(ENTRY))) = (ENTRY)v;
+            }
+        } else if (!any_ovf) {  // buckets past 4 GiB: entry indices, 64-bit addresses
+            uint32_t j = tid;
+            for (; j + 3 * NT < total; j += 4 * NT) {
+                uint32_t v[4], g[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) g[u] = GX[v[u] >> tc.ts];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) buckets[(uint32_t)(g[u] + j + u * NT)] = (ENTRY)v[u];
+            }
+            for (; j < total; j += NT) {
+                const uint32_t v = sorted[j];
+                buckets[(uint32_t)(GX[v >> tc.ts] + j)] = (ENTRY)v;
+            }
+        } else {
+            // overflow: entries past a bucket's capacity go to the spill bitmap
+            for (uint32_t j = tid; j < total; j += NT) {
+                const uint32_t v = sorted[j], t = v >> tc.ts;
+                if (j < S4[t]) {
+                    buckets[(uint32_t)(GX[t] + j)] = (ENTRY)v;
+                } else {
+                    __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                    sc.spill_flag[v >> tc.fts] = 1u;
+                }
             }
         }
     }
@@ -799,192 +844,206 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     }
     __syncthreads();
     if (NB_DIAG_STOP(1)) return;
-    if (sizeof(ENTRY) == 8 || (NB_TWO_TILE && KR > 0 && T <= 2 * NT)) {  // block-uniform:
-        // the common case (C2: T = 1 463); packed entries (host-checked T <= 2 NT, KR > 0) always
+    if constexpr (pack_of<ENTRY>() > 1) {  // packed entries (host-checked T <= 2 NT, KR > 0)
         bin_tail_two_tiles<NT, KPT, kR>(lds, bin_sort_offset_words(T), tc, sc, buckets, base, n,
                                         c.k, ridx, rank);
-        return;
-    }
-
-    // phase 2: block-local run starts; reserve a run in every touched tile's
-    // bucket shard (cursor shard = blockIdx % G, laid out [shard][tile]).  Per tile
-    // the write-out needs only two words afterwards: G[t] := global entry index of
-    // the block's run minus S[t] (u32 wrap-around arithmetic), S[t] := first local
-    // position past the bucket's capacity.
-    if (KR > 0) {  // packed counters (see phase 1) back to counts
-        for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << 16)) >> 2;
-        __syncthreads();
-    }
-    const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
-    const uint32_t shard = blockIdx.x & (tc.G - 1);
-    uint32_t *cur = sc.gcur + (size_t)shard * T;
-    // tiles owned by this thread in phase 2: t = tid + u*NT
-    constexpr int kTPT = (kMaxTiles + NT - 1) / NT;
-    uint32_t gres[kTPT], hcnt[kTPT], gl_g[kTPT], gl_l[kTPT];
-#pragma unroll
-    for (int u = 0; u < kTPT; ++u) {
-        const uint32_t t = tid + u * NT;
-        hcnt[u] = t < T ? cnt[t] : 0u;
-        gres[u] = hcnt[u] ? atomicAdd(&cur[t], hcnt[u]) : 0u;
-    }
-    if (NB_DIAG_STOP(2)) return;
-    // The {G, limit} pair of a tile: G = global entry index of the block's run
-    // minus its local start (u32 wrap-around), limit = first local position past
-    // the bucket's capacity.  `ovf` notes a run that does not fit its bucket.
-    int ovf = 0;
-    auto run_pair = [&](int u, uint32_t t) {
-        const uint32_t st = S[t], g = gres[u];
-        gl_g[u] = (t * tc.G + shard) * tc.cap + g - st;
-        gl_l[u] = st + (g < tc.cap ? tc.cap - g : 0u);
-        ovf |= (uint64_t)g + hcnt[u] > tc.cap;
-    };
-    if (KR > 0) {
-        // phase 3, rank mode: each index goes to its tile's run start + rank; the
-        // reservations' round trips overlap this LDS placement
-#pragma unroll
-        for (int p = 0; p < KPT; ++p) {
-            const uint64_t i = base + (uint64_t)p * NT + tid;
-            if (i < n) {
-#pragma unroll
-                for (int j = 0; j < kR; ++j)
-                    if (j < (int)c.k)
-                        sorted[S[ridx[p][j] >> tc.ts] + ((rank[p][j] & 0xffffu) >> 2)] = ridx[p][j];
-            }
+    } else {
+        if (NB_TWO_TILE && KR > 0 && T <= 2 * NT) {  // block-uniform: the common case (C2)
+            bin_tail_two_tiles<NT, KPT, kR>(lds, bin_sort_offset_words(T), tc, sc, buckets, base,
+                                            n, c.k, ridx, rank);
+            return;
         }
+
+        // phase 2: block-local run starts; reserve a run in every touched tile's
+        // bucket shard (cursor shard = blockIdx % G, laid out [shard][tile]).  Per tile
+        // the write-out needs only two words afterwards: G[t] := global entry index of
+        // the block's run minus S[t] (u32 wrap-around arithmetic), S[t] := first local
+        // position past the bucket's capacity.
+        if (KR > 0) {  // packed counters (see phase 1) back to counts
+            for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << 16)) >> 2;
+            __syncthreads();
+        }
+        const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
+        const uint32_t shard = blockIdx.x & (tc.G - 1);
+        uint32_t *cur = sc.gcur + (size_t)shard * T;
+        // tiles owned by this thread in phase 2: t = tid + u*NT
+        constexpr int kTPT = (kMaxTiles + NT - 1) / NT;
+        uint32_t gres[kTPT], hcnt[kTPT], gl_g[kTPT], gl_l[kTPT];
 #pragma unroll
         for (int u = 0; u < kTPT; ++u) {
             const uint32_t t = tid + u * NT;
-            if (t < T) run_pair(u, t);
+            hcnt[u] = t < T ? cnt[t] : 0u;
+            gres[u] = hcnt[u] ? atomicAdd(&cur[t], hcnt[u]) : 0u;
         }
-    } else {
-        // phase 3, k > 16: regenerate the indices and counting-sort them with
-        // cursor atomics (all k of a key issued before their results are consumed)
+        if (NB_DIAG_STOP(2)) return;
+        // The {G, limit} pair of a tile: G = global entry index of the block's run
+        // minus its local start (u32 wrap-around), limit = first local position past
+        // the bucket's capacity.  `ovf` notes a run that does not fit its bucket.
+        int ovf = 0;
+        auto run_pair = [&](int u, uint32_t t) {
+            const uint32_t st = S[t], g = gres[u];
+            gl_g[u] = (t * tc.G + shard) * tc.cap + g - st;
+            gl_l[u] = st + (g < tc.cap ? tc.cap - g : 0u);
+            ovf |= (uint64_t)g + hcnt[u] > tc.cap;
+        };
+        if (KR > 0) {
+            // phase 3, rank mode: each index goes to its tile's run start + rank; the
+            // reservations' round trips overlap this LDS placement
+#pragma unroll
+            for (int p = 0; p < KPT; ++p) {
+                const uint64_t i = base + (uint64_t)p * NT + tid;
+                if (i < n) {
+#pragma unroll
+                    for (int j = 0; j < kR; ++j)
+                        if (j < (int)c.k)
+                            sorted[S[ridx[p][j] >> tc.ts] + ((rank[p][j] & 0xffffu) >> 2)] = ridx[p][j];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kTPT; ++u) {
+                const uint32_t t = tid + u * NT;
+                if (t < T) run_pair(u, t);
+            }
+        } else {
+            // phase 3, k > 16: regenerate the indices and counting-sort them with
+            // cursor atomics (all k of a key issued before their results are consumed)
+#pragma unroll
+            for (int u = 0; u < kTPT; ++u) {
+                const uint32_t t = tid + u * NT;
+                if (t < T) {
+                    run_pair(u, t);
+                    cnt[t] = S[t];  // placement cursor
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int p = 0; p < KPT; ++p) {
+                const uint64_t i = base + (uint64_t)p * NT + tid;
+                if (i < n) {
+                    IndexGen g = gen[p];
+                    uint32_t j = 0;
+                    for (; j + 4 <= c.k; j += 4) {
+                        uint32_t r[4], q[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            if (j + u) g.next(c);
+                            r[u] = g.r;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) q[u] = atomicAdd(&cnt[r[u] >> tc.ts], 1u);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) sorted[q[u]] = r[u];
+                    }
+                    for (; j < c.k; ++j) {
+                        if (j) g.next(c);
+                        sorted[atomicAdd(&cnt[g.r >> tc.ts], 1u)] = g.r;
+                    }
+                }
+            }
+        }
+        // cnt and S are dead: the run table goes over them.  Every run fits its bucket
+        // unless the input is pathological (massively duplicated keys): then the
+        // table holds {G, limit} pairs and the write-out checks each entry.
+        const bool any_ovf = block_any(ovf, wave_sums + NT / 64 + 1);  // block-uniform
+        uint32_t *GX = lds;  // [T] G only, when nothing overflows
 #pragma unroll
         for (int u = 0; u < kTPT; ++u) {
             const uint32_t t = tid + u * NT;
             if (t < T) {
-                run_pair(u, t);
-                cnt[t] = S[t];  // placement cursor
+                if (any_ovf) GL[t] = make_uint2(gl_g[u], gl_l[u]);
+                else GX[t] = gl_g[u];
             }
         }
         __syncthreads();
-#pragma unroll
-        for (int p = 0; p < KPT; ++p) {
-            const uint64_t i = base + (uint64_t)p * NT + tid;
-            if (i < n) {
-                IndexGen g = gen[p];
-                uint32_t j = 0;
-                for (; j + 4 <= c.k; j += 4) {
-                    uint32_t r[4], q[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        if (j + u) g.next(c);
-                        r[u] = g.r;
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) q[u] = atomicAdd(&cnt[r[u] >> tc.ts], 1u);
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) sorted[q[u]] = r[u];
-                }
-                for (; j < c.k; ++j) {
-                    if (j) g.next(c);
-                    sorted[atomicAdd(&cnt[g.r >> tc.ts], 1u)] = g.r;
-                }
-            }
-        }
-    }
-    // cnt and S are dead: the run table goes over them.  Every run fits its bucket
-    // unless the input is pathological (massively duplicated keys): then the
-    // table holds {G, limit} pairs and the write-out checks each entry.
-    const bool any_ovf = block_any(ovf, wave_sums + NT / 64 + 1);  // block-uniform
-    uint32_t *GX = lds;  // [T] G only, when nothing overflows
-#pragma unroll
-    for (int u = 0; u < kTPT; ++u) {
-        const uint32_t t = tid + u * NT;
-        if (t < T) {
-            if (any_ovf) GL[t] = make_uint2(gl_g[u], gl_l[u]);
-            else GX[t] = gl_g[u];
-        }
-    }
-    __syncthreads();
-    if (NB_DIAG_STOP(3)) return;
+        if (NB_DIAG_STOP(3)) return;
 
-    // phase 4: coalesced write-out of the runs, four independent entries per
-    // lane per step so the LDS lookups overlap.  Entries are stored unmasked (a
-    // u16 store keeps the low bits; the tile kernel masks).
-    if (!any_ovf) {
+        // phase 4: coalesced write-out of the runs, four independent entries per
+        // lane per step so the LDS lookups overlap.  Entries are stored unmasked (a
+        // u16 store keeps the low bits; the tile kernel masks).
+        if (!any_ovf) {
+            uint32_t j = tid;
+            for (; j + 3 * NT < total; j += 4 * NT) {
+                uint32_t v[4], g[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) g[u] = GX[v[u] >> tc.ts];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) buckets[g[u] + j + u * NT] = (ENTRY)v[u];
+            }
+            for (; j < total; j += NT) {
+                const uint32_t v = sorted[j];
+                buckets[GX[v >> tc.ts] + j] = (ENTRY)v;
+            }
+            return;
+        }
+        // slow path: entries past a bucket's capacity go to the spill bitmap
+        auto emit = [&](uint32_t j, uint32_t v, uint2 gl) {
+            if (j < gl.y) {
+                buckets[gl.x + j] = (ENTRY)v;
+            } else {
+                __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+                sc.spill_flag[v >> tc.fts] = 1u;
+            }
+        };
         uint32_t j = tid;
         for (; j + 3 * NT < total; j += 4 * NT) {
-            uint32_t v[4], g[4];
+            uint32_t v[4];
+            uint2 gl[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) g[u] = GX[v[u] >> tc.ts];
+            for (int u = 0; u < 4; ++u) gl[u] = GL[v[u] >> tc.ts];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) buckets[g[u] + j + u * NT] = (ENTRY)v[u];
+            for (int u = 0; u < 4; ++u) emit(j + u * NT, v[u], gl[u]);
         }
         for (; j < total; j += NT) {
             const uint32_t v = sorted[j];
-            buckets[GX[v >> tc.ts] + j] = (ENTRY)v;
+            emit(j, v, GL[v >> tc.ts]);
         }
-        return;
-    }
-    // slow path: entries past a bucket's capacity go to the spill bitmap
-    auto emit = [&](uint32_t j, uint32_t v, uint2 gl) {
-        if (j < gl.y) {
-            buckets[gl.x + j] = (ENTRY)v;
-        } else {
-            __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
-            sc.spill_flag[v >> tc.fts] = 1u;
-        }
-    };
-    uint32_t j = tid;
-    for (; j + 3 * NT < total; j += 4 * NT) {
-        uint32_t v[4];
-        uint2 gl[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) gl[u] = GL[v[u] >> tc.ts];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) emit(j + u * NT, v[u], gl[u]);
-    }
-    for (; j < total; j += NT) {
-        const uint32_t v = sorted[j];
-        emit(j, v, GL[v >> tc.ts]);
     }
 }
 
 // Two-level build for very large filters (T > 2 NT fine tiles, e.g. C5's 4 096
 // tiles of 2^20 bits): binned straight into fine tiles, a block's 1 024 keys x k
 // indices spread over T tiles make runs of ~2.5 entries -- every run a separate
-// reservation atomic and L2 write request.  Pass 1 (the bin kernel with 2^(ts+6)-bit
-// super tiles, full 32-bit indices) makes runs of ~k x 1 024 / T1; pass 2 (this
-// kernel) re-bins each super tile's entries into its 64 fine tiles by an LDS
-// counting sort over 16 384 entries per block (runs of ~256); pass 3 is the tile
-// kernel on the fine tiles.  One extra read + write of the entries buys runs two
-// orders of magnitude longer.  grid = (blocks per super tile, super tiles).
-constexpr uint32_t kSuperFine = 64;  // fine tiles per super tile
-constexpr uint32_t kMaxSuper = 64;   // super tiles (m < 2^32 with 2^26-bit super tiles)
+// reservation atomic and L2 write request.  Pass 1 (the bin kernel on super tiles
+// of 2^(ts+5) bits, entries packed five 25-bit in-super-tile offsets per 16 bytes
+// (Pack5); or, with NB_PACK5=0 / k > 16, 2^(ts+6)-bit super tiles and full 32-bit
+// indices) makes runs of ~k x 1 024 / T1; pass 2 (this kernel) re-bins each super
+// tile's entries into its 32 (64) fine tiles by an LDS counting sort over ~16k
+// entries per block (runs of ~500 (256)); pass 3 is the tile kernel on the fine
+// tiles.  One extra read + write of the entries buys runs two orders of magnitude
+// longer.  grid = (blocks per super tile, super tiles).
+constexpr uint32_t kSuperFine = 64;  // fine tiles per super tile (at most)
+constexpr uint32_t kMaxSuper = 128;  // super tiles (m < 2^32 with 2^25-bit super tiles)
 constexpr int kRebinThreads = 1024;
-constexpr int kRebinEPT = 16;        // entries per thread
-constexpr uint32_t kRebinSpan = kRebinThreads * kRebinEPT;
+// entries per thread: 16 32-bit entries, or three Pack5 units (15 entries)
+template <bool IN5>
+__host__ __device__ constexpr uint32_t rebin_ept() { return IN5 ? 15u : 16u; }
+template <bool IN5>
+__host__ __device__ constexpr uint32_t rebin_span() { return kRebinThreads * rebin_ept<IN5>(); }
 
 // PACK: fine entries three per 64-bit word (runs padded to a multiple of 3 slots
 // with copies of their first entry, as in bin_tail_two_tiles); capacities,
-// cursors and the run table in words.
-template <bool PACK>
+// cursors and the run table in words.  IN5: pass-1 buckets of Pack5 units
+// (cursors, capacities in units; their pad slots are copies of real entries,
+// re-binned like any other).
+template <bool PACK, bool IN5>
 __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
-    TileCfg t1, TileCfg t2, TileScratch sc1, TileScratch sc2, const uint32_t *__restrict__ b1,
+    TileCfg t1, TileCfg t2, TileScratch sc1, TileScratch sc2, const void *__restrict__ b1v,
     void *__restrict__ b2v) {
+    constexpr uint32_t EPT = rebin_ept<IN5>(), UPT = IN5 ? EPT / 5 : EPT;  // units per thread
+    constexpr uint32_t kSpanUnits = kRebinThreads * UPT;
     __shared__ uint32_t v0[kShards + 1];
     __shared__ uint32_t fcnt[kSuperFine], fS[kSuperFine], fGX[kSuperFine], flim[kSuperFine];
     __shared__ uint32_t slot_total;
     __shared__ int any_ovf;
     uint32_t *b2 = reinterpret_cast<uint32_t *>(b2v);
-    extern __shared__ uint32_t sorted[];  // [kRebinSpan]
+    extern __shared__ uint32_t sorted[];  // [rebin_span + pads]
     const uint32_t tid = threadIdx.x, s = blockIdx.y;
+    const uint32_t nfine = 1u << (t1.ts - t2.ts);  // fine tiles per super tile (<= 64)
     if (tid == 0) {
         uint32_t acc = 0;
         for (uint32_t g = 0; g < t1.G; ++g) {
@@ -996,28 +1055,41 @@ __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
     }
     if (tid < kSuperFine) fcnt[tid] = 0;
     __syncthreads();
-    const uint32_t total = v0[t1.G];
-    const uint32_t first = blockIdx.x * kRebinSpan;
+    const uint32_t total = v0[t1.G];  // units
+    const uint32_t first = blockIdx.x * kSpanUnits;
     if (first >= total) return;  // block-uniform
-    const uint32_t cnt = min(kRebinSpan, total - first);
-    const uint32_t fbase = s * kSuperFine;  // first fine tile of super tile s
+    const uint32_t cntu = min(kSpanUnits, total - first);
+    const uint32_t fbase = s * nfine;  // first fine tile of super tile s
     // load this block's entries (the G shards as one flat range), count per fine tile
-    uint32_t v[kRebinEPT], r[kRebinEPT];
+    uint32_t v[EPT], r[EPT];
     uint32_t g = 0;
 #pragma unroll
-    for (int u = 0; u < kRebinEPT; ++u) {
+    for (uint32_t u = 0; u < UPT; ++u) {
         const uint32_t q = first + tid + u * kRebinThreads;
-        if (q < first + cnt) {
+        if (q < first + cntu) {
             while (g + 1 < t1.G && q >= v0[g + 1]) ++g;
-            v[u] = b1[(size_t)(s * t1.G + g) * t1.cap + (q - v0[g])];
+            const size_t at = (size_t)(s * t1.G + g) * t1.cap + (q - v0[g]);
+            if constexpr (IN5) {
+                const Pack5 p = reinterpret_cast<const Pack5 *>(b1v)[at];
+                const uint32_t msk = (1u << 25) - 1, sb = s << t1.ts;
+                v[5 * u + 0] = sb | (p.x & msk);
+                v[5 * u + 1] = sb | (((p.x >> 25) | (p.y << 7)) & msk);
+                v[5 * u + 2] = sb | (((p.y >> 18) | (p.z << 14)) & msk);
+                v[5 * u + 3] = sb | (((p.z >> 11) | (p.w << 21)) & msk);
+                v[5 * u + 4] = sb | (p.w >> 4);
+            } else {
+                v[u] = reinterpret_cast<const uint32_t *>(b1v)[at];
+            }
         }
     }
+    // entry e of the thread is valid while its unit is
+    auto valid = [&](uint32_t e) { return tid + (IN5 ? e / 5 : e) * kRebinThreads < cntu; };
 #pragma unroll
-    for (int u = 0; u < kRebinEPT; ++u)
-        if (tid + u * kRebinThreads < cnt) r[u] = atomicAdd(&fcnt[(v[u] >> t2.ts) - fbase], 1u);
+    for (uint32_t e = 0; e < EPT; ++e)
+        if (valid(e)) r[e] = atomicAdd(&fcnt[(v[e] >> t2.ts) - fbase], 1u);
     __syncthreads();
-    if (tid < kSuperFine) {  // wave 0: scan the 64 counts, reserve the 64 runs
-        const uint32_t c = fcnt[tid];
+    if (tid < kSuperFine) {  // wave 0: scan the fine tiles' counts, reserve their runs
+        const uint32_t c = tid < nfine ? fcnt[tid] : 0u;
         const uint32_t sl = PACK ? (c + 2) / 3 * 3 : c, u = PACK ? sl / 3 : c;
         const uint32_t incl = wave_inclusive_scan(sl), st = incl - sl;
         if (tid == kSuperFine - 1) slot_total = incl;
@@ -1032,8 +1104,8 @@ __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
     }
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < kRebinEPT; ++u)
-        if (tid + u * kRebinThreads < cnt) sorted[fS[(v[u] >> t2.ts) - fbase] + r[u]] = v[u];
+    for (uint32_t e = 0; e < EPT; ++e)
+        if (valid(e)) sorted[fS[(v[e] >> t2.ts) - fbase] + r[e]] = v[e];
     __syncthreads();
     const bool ovf = any_ovf != 0;
     if constexpr (PACK) {
@@ -1061,7 +1133,7 @@ __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
         }
         return;
     }
-    for (uint32_t j = tid; j < cnt; j += kRebinThreads) {
+    for (uint32_t j = tid; j < slot_total; j += kRebinThreads) {
         const uint32_t x = sorted[j], f = (x >> t2.ts) - fbase;
         if (!ovf || j < flim[f]) {
             b2[fGX[f] + j] = x;
@@ -1361,9 +1433,10 @@ TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
 }
 
 // Pass 1 of the two-level build: super tiles of kSuperFine fine tiles each.
-TileCfg super_tiles(const TileCfg &fine, uint32_t m, uint64_t n_chunk, uint32_t k) {
+TileCfg super_tiles(const TileCfg &fine, uint32_t m, uint64_t n_chunk, uint32_t k,
+                    uint32_t fine_log2) {
     TileCfg tc = fine;
-    tc.ts = fine.ts + 6;  // log2(kSuperFine)
+    tc.ts = fine.ts + fine_log2;  // 2^fine_log2 fine tiles per super tile
     tc.T = (uint32_t)(((uint64_t)m + (1ull << tc.ts) - 1) >> tc.ts);
     const double e = (double)n_chunk * k / ((double)tc.T * tc.G);
     uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
@@ -1459,19 +1532,35 @@ void (*tile_kernel_of())(TileCfg, TileScratch, const void *, uint64_t *, uint64_
         bloom_tile_or_kernel<ENTRY, OVERWRITE>);
 }
 
+// Pass-1 entry type of the two-level build: Pack5 units (k <= 16, the rank-mode
+// tail; NB_PACK5=0 for the A/B) or 32-bit indices.
+bool two_level_pack5() { return env_u32("NB_PACK5", 1) != 0; }
+
 // The two-level build (see bloom_rebin_kernel): per chunk, the bin kernel into
 // super tiles, the re-bin into fine tiles, the tile kernel on the fine tiles.
-template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR>
+// E1: pass-1 entry type (Pack5 or uint32_t); t1 comes with its capacity in entries.
+template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR, typename E1>
 int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                      const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st,
-                     uint64_t chunk, const TileCfg &t1, const TileCfg &t2) {
+                     uint64_t chunk, const TileCfg &t1e, const TileCfg &t2) {
     constexpr uint64_t kpb = (uint64_t)KPT * NT;
+    constexpr bool IN5 = pack_of<E1>() == 5;
     Workspace *ws;
     TileScratch sc;
     int rc;
     if ((rc = get_ws(st, &ws))) return rc;
     std::lock_guard<std::mutex> lk(ws->mu);
-    const uint32_t rebin_x = (uint32_t)(((uint64_t)t1.cap * t1.G + kRebinSpan - 1) / kRebinSpan);
+    // pass-1 capacity in units: the entries' plus <= 4 pad slots per bin block of
+    // the shard, / 5
+    const uint64_t nblk = (chunk + kpb - 1) / kpb;
+    TileCfg t1 = t1e;
+    if (IN5) {
+        const uint64_t bps = (nblk + t1.G - 1) / t1.G;
+        const uint64_t capu = ((uint64_t)t1.cap + 4 * bps + 4) / 5;
+        t1.cap = (uint32_t)std::min<uint64_t>((capu + 7) & ~7ull, 0xFFFFFFC0ull);
+    }
+    const uint32_t span_units = kRebinThreads * (IN5 ? rebin_ept<true>() / 5 : rebin_ept<false>());
+    const uint32_t rebin_x = (uint32_t)(((uint64_t)t1.cap * t1.G + span_units - 1) / span_units);
     // fine entries packed three per word (2^ts2 <= 2^21): capacity in words, the
     // entries' plus <= 2 pad slots per re-bin block of the shard
     const bool pack = t2.ts <= 20 && env_u32("NB_PACK", 1) != 0;
@@ -1482,18 +1571,19 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
         t2p.cap = (uint32_t)std::min<uint64_t>((capw + 7) & ~7ull, 0xFFFFFFC0ull);
     }
     const size_t e2 = pack ? 8 : 4;
-    if ((rc = ws_reserve(*ws, c.fm.m, (size_t)t1.T * t1.G * t1.cap * 4, &sc,
+    if ((rc = ws_reserve(*ws, c.fm.m, (size_t)t1.T * t1.G * t1.cap * sizeof(E1), &sc,
                          (size_t)t2p.T * t2p.G * t2p.cap * e2)))
         return rc;
     TileScratch sc1 = sc;
     sc1.gcur = super_cursors(*ws);
     size_t sort_bytes = kpb * c.k * 4;
+    if (IN5) sort_bytes += (size_t)t1.T * 16;  // <= 4 pad slots per run
     if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(NT));
     const size_t bin_lds = (size_t)bin_sort_offset_words(t1.T) * 4 + sort_bytes;
-    const size_t rebin_lds = ((size_t)kRebinSpan + 2 * kSuperFine) * 4;
+    const size_t rebin_lds = ((size_t)rebin_span<IN5>() + 2 * kSuperFine) * 4;
     const size_t tile_lds = ((size_t)1 << (t2.ts - 3)) + (2 * kShards + 1) * 4;
-    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, uint32_t, NT, STAGE, KR>;
-    auto rebin = pack ? bloom_rebin_kernel<true> : bloom_rebin_kernel<false>;
+    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, E1, NT, STAGE, KR>;
+    auto rebin = pack ? bloom_rebin_kernel<true, IN5> : bloom_rebin_kernel<false, IN5>;
     auto tile_ow = pack ? tile_kernel_of<uint64_t, true>() : tile_kernel_of<uint32_t, true>();
     auto tile_or = pack ? tile_kernel_of<uint64_t, false>() : tile_kernel_of<uint32_t, false>();
     if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(tile_ow, tile_lds)) ||
@@ -1502,7 +1592,7 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
     NB_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(rebin),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rebin_lds));
     const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
-    uint32_t *b1 = reinterpret_cast<uint32_t *>(ws->buckets);
+    E1 *b1 = reinterpret_cast<E1 *>(ws->buckets);
     void *b2 = ws->buckets2;
     for (uint64_t done = 0; done < n; done += chunk) {
         const uint64_t cn = std::min(chunk, n - done);
@@ -1512,7 +1602,7 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
                            co, key_len, cn, c, t1, sc1, b1);
         NB_HIP(hipGetLastError());
         hipLaunchKernelGGL(rebin, dim3(rebin_x, t1.T), dim3(kRebinThreads), rebin_lds,
-                           st, t1, t2p, sc1, sc, b1, b2);
+                           st, t1, t2p, sc1, sc, (const void *)b1, b2);
         NB_HIP(hipGetLastError());
         NB_HIP(hipMemsetAsync(sc1.gcur, 0, (size_t)t1.G * t1.T * 4, st));  // keep them zero
         hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(t2.T),
@@ -1535,9 +1625,15 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
         chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, (n + passes - 1) / passes));
         if (const uint64_t v = env_u32("NB_CHUNK_KEYS", 0)) chunk = std::min<uint64_t>(n, v);
         tc = choose_tiles(c.fm.m, chunk, c.k);
-        return launch_two_level<FLAVOR, LAYOUT, KPT, NT, STAGE, KR>(
+        if constexpr (KR > 0) {
+            if (two_level_pack5())  // 2^(ts+5)-bit super tiles: 25-bit offsets
+                return launch_two_level<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, Pack5>(
+                    keys, offsets, key_len, n, c, words, overwrite, st, chunk,
+                    super_tiles(tc, c.fm.m, chunk, c.k, 5), tc);
+        }
+        return launch_two_level<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, uint32_t>(
             keys, offsets, key_len, n, c, words, overwrite, st, chunk,
-            super_tiles(tc, c.fm.m, chunk, c.k), tc);
+            super_tiles(tc, c.fm.m, chunk, c.k, 6), tc);
     }
     if (tc.ts <= 16 && env_u32("NB_ENTRY32", 0) == 0)
         return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint16_t, NT, STAGE, KR>(
