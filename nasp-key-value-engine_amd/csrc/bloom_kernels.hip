@@ -329,6 +329,29 @@ constexpr uint32_t kMaxTiles = 4096;
 #ifndef NB_DIAG_NOCOUNT
 #define NB_DIAG_NOCOUNT false
 #endif
+// Cache policy of the bucket round trip (A/B knobs): non-temporal bucket-word
+// stores in the bin kernel's write-out (2x slower: runs are partial lines that the
+// L2 otherwise merges), non-temporal bucket loads in the tile and re-bin kernels
+// (read once; on by default).  Non-temporal key loads in the bin kernel measured
+// 0.5-1 % slower (C3/C4/C5) and are not used.
+#ifndef NB_NT_STORE
+#define NB_NT_STORE 0
+#endif
+#ifndef NB_NT_LOAD
+#define NB_NT_LOAD 1  // C4 1.538-1.564 -> 1.527-1.535 ms, C2 0.148 -> 0.144 (same-box A/Bs)
+#endif
+__device__ __forceinline__ void bucket_store(uint64_t *p, uint64_t v) {
+    if (NB_NT_STORE) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 bucket_load(const uint4 *p) {
+    if (NB_NT_LOAD) {
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
+    return *p;
+}
 
 // Inclusive prefix sum across a wave64 with DPP row shifts and the GFX9 row
 // broadcasts (6 VALU ops, no LDS round trips): Hillis-Steele inside each 16-lane
@@ -580,12 +603,13 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
                 for (int u = 0; u < 2; ++u) w[u] = word_at(q + u * NT, &t[u]);
 #pragma unroll
                 for (int u = 0; u < 2; ++u)
-                    *reinterpret_cast<uint64_t *>(bb + (GX[t[u]] + (q + u * NT) * 8u)) = w[u];
+                    bucket_store(reinterpret_cast<uint64_t *>(bb + (GX[t[u]] + (q + u * NT) * 8u)),
+                                 w[u]);
             }
             for (; q < words; q += NT) {
                 uint32_t t;
                 const uint64_t w = word_at(q, &t);
-                *reinterpret_cast<uint64_t *>(bb + (GX[t] + q * 8u)) = w;
+                bucket_store(reinterpret_cast<uint64_t *>(bb + (GX[t] + q * 8u)), w);
             }
         } else {
             uint64_t *bw = reinterpret_cast<uint64_t *>(buckets);
@@ -1070,7 +1094,7 @@ __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
             while (g + 1 < t1.G && q >= v0[g + 1]) ++g;
             const size_t at = (size_t)(s * t1.G + g) * t1.cap + (q - v0[g]);
             if constexpr (IN5) {
-                const Pack5 p = reinterpret_cast<const Pack5 *>(b1v)[at];
+                const uint4 p = bucket_load(reinterpret_cast<const uint4 *>(b1v) + at);
                 const uint32_t msk = (1u << 25) - 1, sb = s << t1.ts;
                 v[5 * u + 0] = sb | (p.x & msk);
                 v[5 * u + 1] = sb | (((p.x >> 25) | (p.y << 7)) & msk);
@@ -1195,7 +1219,7 @@ __global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
     auto vec_at = [&](uint32_t v) {
         while (g + 1 < tc.G && v >= shard_v0[g + 1]) ++g;
         const uint4 *ev = reinterpret_cast<const uint4 *>(tile_base + (size_t)g * tc.cap);
-        return ev[v - shard_v0[g]];
+        return bucket_load(ev + (v - shard_v0[g]));
     };
     uint32_t q = tid;
     for (; q + (UNROLL - 1) * NT < nvec; q += UNROLL * NT) {
