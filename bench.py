@@ -485,7 +485,7 @@ def bench_merkle(args, world, rank, dev):
 def bench_cooperative(args, wl, world, rank, dev):
     """C5: 1B x 32B keys, k=10, m=2^32-1, one filter built by all ranks: each rank
     builds a full-size partial filter from its key range, then the all-to-all +
-    OR-merge + all-gather (nasp_bloom.distributed).  Keys are generated on the
+    OR-merge + all-gather (nasp_bloom.distributed; one rank: no collective).  Keys are generated on the
     device (32 GB in total) -- only the build is timed."""
     import torch
     import torch.distributed as dist
@@ -535,8 +535,9 @@ def bench_cooperative(args, wl, world, rank, dev):
            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
            "data": "synthetic (device-generated random 32-byte keys)",
            "config": {"workload": wl.name, "keys_total": wl.n, "key_bytes": wl.key_len, "m": wl.m,
-                      "k": wl.k, "h2_seed": seed, "parallelism": f"cooperative x{world}: "
-                      "key shards + all-to-all OR reduce-scatter + all-gather"},
+                      "k": wl.k, "h2_seed": seed, "parallelism": (f"cooperative x{world}: key shards + all-to-all OR "
+                                      "reduce-scatter + all-gather") if world > 1 else
+                      "one rank: its partial is the whole filter, no collective"},
            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
                         "kernel": "whole cooperative step per GPU (build + merge collectives)"}}

@@ -50,14 +50,18 @@ def _hip_merge(dst: torch.Tensor, recv: torch.Tensor, nsrc: int, stride: int) ->
 
 
 def merge_partials(partial: torch.Tensor, m: int, group=None, all_gather: bool = True,
-                   merge_fn: Callable | None = None) -> torch.Tensor:
+                   merge_fn: Callable | None = None, exchange_single: bool = False) -> torch.Tensor:
     """OR-merge every rank's full-size partial filter (int64 tensor of >= world*S
     words, padding zero).  Returns the whole merged filter (all_gather=True) or this
-    rank's owned slice of S words."""
+    rank's owned slice of S words.  With one rank the partial already is the filter
+    and no collective runs (exchange_single=True forces the all-to-all / OR /
+    all-gather sequence anyway, for tests of the RCCL path on a one-GPU box)."""
     world = dist.get_world_size(group)
     S = slice_words(m, world)
     if partial.numel() < world * S:
         raise ValueError("partial filter must be padded to world * slice_words(m) words")
+    if world == 1 and not exchange_single:
+        return partial[:S]
     send = partial[: world * S].contiguous()
     recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send, group=group)          # recv[j*S:(j+1)*S] = slice of rank j
@@ -73,7 +77,8 @@ def merge_partials(partial: torch.Tensor, m: int, group=None, all_gather: bool =
 def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len: int, n: int,
                       m: int, k: int, seed: int, flavor: int, group=None,
                       all_gather: bool = True, build_fn: Callable | None = None,
-                      merge_fn: Callable | None = None, stream=None) -> torch.Tensor:
+                      merge_fn: Callable | None = None, stream=None,
+                      exchange_single: bool = False) -> torch.Tensor:
     """Cooperative single-filter build.  `keys`/`offsets` hold THIS rank's key range
     (offsets relative to `keys`, n+1 entries; or fixed key_len).  Every rank passes
     the same (m, k, seed, flavor)."""
@@ -90,7 +95,8 @@ def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len:
                      overwrite=True)
     else:
         build_fn(keys, offsets, key_len, n, m, k, seed, flavor, partial)
-    return merge_partials(partial, m, group=group, all_gather=all_gather, merge_fn=merge_fn)
+    return merge_partials(partial, m, group=group, all_gather=all_gather, merge_fn=merge_fn,
+                          exchange_single=exchange_single)
 
 
 def build_independent(keys: torch.Tensor, offsets: torch.Tensor | None, key_len: int, n: int,

@@ -730,7 +730,8 @@ def test_or_merge_kernel(dev):
 
 def test_cooperative_build_single_rank(dev, oracle):
     """The cooperative (C5) path end to end on one GPU through RCCL (world size 1):
-    partial build + all-to-all + HIP OR-merge + all-gather."""
+    partial build + all-to-all + HIP OR-merge + all-gather (forced), and the
+    one-rank shortcut that returns the partial itself."""
     import os
     import torch
     import torch.distributed as dist
@@ -742,9 +743,11 @@ def test_cooperative_build_single_rank(dev, oracle):
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
     n = 1_000_000
     buf = synth.fixed_keys(n, 32)
-    full = D.build_cooperative(t_u8(buf, dev), None, 32, n, synth.C5.m, synth.C5.k, SEED, 0)
-    torch.cuda.synchronize()
     want = oracle.build(0, buf, None, 32, n, synth.C5.m, synth.C5.k, SEED)
-    got = full.cpu().numpy().view(np.uint64)
-    np.testing.assert_array_equal(got[: want.size], want)
+    for exchange in (True, False):  # through RCCL, then the one-rank shortcut
+        full = D.build_cooperative(t_u8(buf, dev), None, 32, n, synth.C5.m, synth.C5.k, SEED, 0,
+                                   exchange_single=exchange)
+        torch.cuda.synchronize()
+        got = full.cpu().numpy().view(np.uint64)
+        np.testing.assert_array_equal(got[: want.size], want)
     dist.destroy_process_group()
