@@ -9,7 +9,7 @@ import csv
 import os
 import sys
 
-N = {"c2": 10e6, "c4": 100e6, "c3": 100e6}
+N = {"c2": 10e6, "c4": 100e6, "c3": 100e6, "c5": 200e6}  # c5: one 200M-key pass
 LABELS = ["hash+index", "+count", "+scan/res", "+placement", "+write-out"]
 
 

@@ -98,9 +98,53 @@ static float time_bin_packed(const uint8_t *keys, uint64_t n, const FilterConsts
     return best;
 }
 
+// C5's pass-1 bin kernel (one 200M-key pass of 32-byte keys, k = 10, m = 2^32-1,
+// Pack5 entries into 2^25-bit super tiles, as launch_two_level configures it), one
+// dispatch per phase stop for per-phase counters (tools/pmc_phase.sh c5).
+static int c5_pmc() {
+    const uint64_t n = 200000000;
+    const uint32_t m = 0xFFFFFFFFu, k = 10;
+    constexpr int NT = kBinThreads, KPT = 1;
+    constexpr uint64_t kpb = (uint64_t)KPT * NT;
+    uint8_t *keys;
+    CK(hipMalloc(&keys, n * 32 + 64));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, reinterpret_cast<uint64_t *>(keys), n * 4);
+    FilterConsts c = nb::make_consts(m, k, 17027509906831645879ull, 0);
+    nb::set_fixed_len(c, 32);
+    TileCfg t1 = super_tiles(choose_tiles(m, n, k), m, n, k, 5);
+    const uint64_t nblk = (n + kpb - 1) / kpb, bps = (nblk + t1.G - 1) / t1.G;
+    const uint64_t capu = ((uint64_t)t1.cap + 4 * bps + 4) / 5;
+    t1.cap = (uint32_t)((capu + 7) & ~7ull);
+    void *buckets;
+    CK(hipMalloc(&buckets, (size_t)t1.T * t1.G * t1.cap * 16));
+    TileScratch sc;
+    uint32_t *zeroed;
+    const size_t zb = (kCurWords + kMaxTiles + 2 * (((size_t)m + 63) / 64)) * 4;
+    CK(hipMalloc(&zeroed, zb));
+    CK(hipMemset(zeroed, 0, zb));
+    sc.gcur = zeroed;
+    sc.spill_flag = zeroed + kCurWords;
+    sc.spill32 = zeroed + kCurWords + kMaxTiles;
+    const size_t lds = (size_t)bin_sort_offset_words(t1.T) * 4 + kpb * k * 4 + (size_t)t1.T * 16;
+    auto kern = bloom_bin_kernel<0, kFixed32, KPT, Pack5, NT, false, 16>;
+    allow_lds(kern, lds);
+    printf("C5 pass 1: ts=%u T=%u G=%u cap=%u units\n", t1.ts, t1.T, t1.G, t1.cap);
+    for (int stop : {11, 1, 2, 3, 0}) {
+        set_stop(stop);
+        CK(hipMemset(sc.gcur, 0, kCurWords * 4));
+        hipLaunchKernelGGL(kern, dim3((uint32_t)nblk), dim3(NT), lds, 0, keys, nullptr, 32u, n, c, t1,
+                           sc, (Pack5 *)buckets);
+        CK(hipDeviceSynchronize());
+    }
+    set_stop(0);
+    printf("pmc dispatches: stops 11 1 2 3 0\n");
+    return 0;
+}
+
 int main(int argc, char **argv) {
     // argv[1]: c2 (default), c4 (the 100M-key shard) or c3 (100M keys of 8-64 bytes);
-    // argv[2] == "intmod": integer remainders
+    // c5 (pmc only): C5's pass-1 bin kernel; argv[2] == "intmod": integer remainders
+    if (argc > 1 && !strcmp(argv[1], "c5")) return c5_pmc();
     const bool c4 = argc > 1 && !strcmp(argv[1], "c4"), c3 = argc > 1 && !strcmp(argv[1], "c3");
     const uint64_t n = (c4 || c3) ? 100000000 : 10000000;
     const uint32_t m = (c4 || c3) ? 958505838u : 95850584u, k = 7;
