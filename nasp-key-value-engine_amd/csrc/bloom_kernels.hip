@@ -385,6 +385,12 @@ __device__ __forceinline__ bool block_any(int pred, uint32_t *flag) {
     return *flag != 0u;
 }
 
+// A workgroup barrier that waits only for the wave's own LDS operations: its global
+// memory operations (e.g. reservation atomics) stay in flight across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // Exclusive scan of hist[0..T) into S[0..T); returns the total.  blockDim = NT.
 template <int NT>
 __device__ uint32_t block_exclusive_scan(const uint32_t *hist, uint32_t *S, uint32_t T,
@@ -1084,26 +1090,31 @@ __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
     if (first >= total) return;  // block-uniform
     const uint32_t cntu = min(kSpanUnits, total - first);
     const uint32_t fbase = s * nfine;  // first fine tile of super tile s
-    // load this block's entries (the G shards as one flat range), count per fine tile
+    // load this block's entries (the G shards as one flat range), count per fine tile.
+    // All UPT loads are issued before any is consumed: a lane past the block's
+    // range reloads its last unit (clamped index, never used), so the loads are
+    // unconditional -- under a per-unit `if` the compiler waited for each load
+    // inside its branch, three exposed HBM latencies per lane.
     uint32_t v[EPT], r[EPT];
+    uint4 p[IN5 ? UPT : 1];
     uint32_t g = 0;
 #pragma unroll
     for (uint32_t u = 0; u < UPT; ++u) {
-        const uint32_t q = first + tid + u * kRebinThreads;
-        if (q < first + cntu) {
-            while (g + 1 < t1.G && q >= v0[g + 1]) ++g;
-            const size_t at = (size_t)(s * t1.G + g) * t1.cap + (q - v0[g]);
-            if constexpr (IN5) {
-                const uint4 p = bucket_load(reinterpret_cast<const uint4 *>(b1v) + at);
-                const uint32_t msk = (1u << 25) - 1, sb = s << t1.ts;
-                v[5 * u + 0] = sb | (p.x & msk);
-                v[5 * u + 1] = sb | (((p.x >> 25) | (p.y << 7)) & msk);
-                v[5 * u + 2] = sb | (((p.y >> 18) | (p.z << 14)) & msk);
-                v[5 * u + 3] = sb | (((p.z >> 11) | (p.w << 21)) & msk);
-                v[5 * u + 4] = sb | (p.w >> 4);
-            } else {
-                v[u] = reinterpret_cast<const uint32_t *>(b1v)[at];
-            }
+        const uint32_t q = min(first + tid + u * kRebinThreads, first + cntu - 1);
+        while (g + 1 < t1.G && q >= v0[g + 1]) ++g;
+        const size_t at = (size_t)(s * t1.G + g) * t1.cap + (q - v0[g]);
+        if constexpr (IN5) p[u] = bucket_load(reinterpret_cast<const uint4 *>(b1v) + at);
+        else v[u] = reinterpret_cast<const uint32_t *>(b1v)[at];
+    }
+    if constexpr (IN5) {
+        const uint32_t msk = (1u << 25) - 1, sb = s << t1.ts;
+#pragma unroll
+        for (uint32_t u = 0; u < UPT; ++u) {
+            v[5 * u + 0] = sb | (p[u].x & msk);
+            v[5 * u + 1] = sb | (((p[u].x >> 25) | (p[u].y << 7)) & msk);
+            v[5 * u + 2] = sb | (((p[u].y >> 18) | (p[u].z << 14)) & msk);
+            v[5 * u + 3] = sb | (((p[u].z >> 11) | (p[u].w << 21)) & msk);
+            v[5 * u + 4] = sb | (p[u].w >> 4);
         }
     }
     // entry e of the thread is valid while its unit is
@@ -1112,32 +1123,44 @@ __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
     for (uint32_t e = 0; e < EPT; ++e)
         if (valid(e)) r[e] = atomicAdd(&fcnt[(v[e] >> t2.ts) - fbase], 1u);
     __syncthreads();
-    if (tid < kSuperFine) {  // wave 0: scan the fine tiles' counts, reserve their runs
+    // wave 0: scan the fine tiles' counts and reserve their runs.  The reservation
+    // atomics stay in flight through the placement (an LDS-only barrier publishes
+    // the run starts); the run table is written after it.
+    uint32_t gr = 0, fu = 0, fstu = 0, fshard = 0;
+    if (tid < kSuperFine) {
         const uint32_t c = tid < nfine ? fcnt[tid] : 0u;
-        const uint32_t sl = PACK ? (c + 2) / 3 * 3 : c, u = PACK ? sl / 3 : c;
+        const uint32_t sl = PACK ? (c + 2) / 3 * 3 : c;
+        fu = PACK ? sl / 3 : c;
         const uint32_t incl = wave_inclusive_scan(sl), st = incl - sl;
         if (tid == kSuperFine - 1) slot_total = incl;
-        const uint32_t t = fbase + tid;
-        const uint32_t shard = (blockIdx.y * gridDim.x + blockIdx.x) & (t2.G - 1);
-        const uint32_t gr = u ? atomicAdd(&sc2.gcur[(size_t)shard * t2.T + t], u) : 0u;
-        const uint32_t stu = PACK ? st / 3 : st;
+        fshard = (blockIdx.y * gridDim.x + blockIdx.x) & (t2.G - 1);
+        gr = fu ? atomicAdd(&sc2.gcur[(size_t)fshard * t2.T + fbase + tid], fu) : 0u;
+        fstu = PACK ? st / 3 : st;
         fS[tid] = st;
-        fGX[tid] = (t * t2.G + shard) * t2.cap + gr - stu;
-        flim[tid] = stu + (gr < t2.cap ? t2.cap - gr : 0u);
-        if ((uint64_t)gr + u > t2.cap) any_ovf = 1;
     }
-    __syncthreads();
+    lds_barrier();
+    // placement; the entry of rank 0 in its fine tile also fills the run's pad
+    // slots (PACK: up to a multiple of 3) with copies of itself
 #pragma unroll
-    for (uint32_t e = 0; e < EPT; ++e)
-        if (valid(e)) sorted[fS[(v[e] >> t2.ts) - fbase] + r[e]] = v[e];
+    for (uint32_t e = 0; e < EPT; ++e) {
+        if (valid(e)) {
+            const uint32_t f = (v[e] >> t2.ts) - fbase, st = fS[f];
+            sorted[st + r[e]] = v[e];
+            if (PACK && r[e] == 0) {
+                const uint32_t c = fcnt[f];
+                for (uint32_t q = c; q < (c + 2) / 3 * 3; ++q) sorted[st + q] = v[e];
+            }
+        }
+    }
+    if (tid < kSuperFine) {
+        const uint32_t t = fbase + tid;
+        fGX[tid] = (t * t2.G + fshard) * t2.cap + gr - fstu;
+        flim[tid] = fstu + (gr < t2.cap ? t2.cap - gr : 0u);
+        if ((uint64_t)gr + fu > t2.cap) any_ovf = 1;
+    }
     __syncthreads();
     const bool ovf = any_ovf != 0;
     if constexpr (PACK) {
-        if (tid < kSuperFine) {  // pad slots: copies of the run's first entry
-            const uint32_t c = fcnt[tid], st = fS[tid];
-            for (uint32_t q = c; q < (c + 2) / 3 * 3; ++q) sorted[st + q] = sorted[st];
-        }
-        __syncthreads();
         uint64_t *bw = reinterpret_cast<uint64_t *>(b2v);
         const uint32_t words = slot_total / 3, msk = (1u << t2.ts) - 1;
         for (uint32_t q = tid; q < words; q += kRebinThreads) {
