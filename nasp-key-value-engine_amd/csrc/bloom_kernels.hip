@@ -1666,8 +1666,10 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
     uint64_t chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, chunk_keys(n, c.k)));
     TileCfg tc = choose_tiles(c.fm.m, chunk, c.k);
     if (tc.T > 2 * (uint32_t)NT && env_u32("NB_TWO_LEVEL", 1) != 0) {
-        // two bucket arrays of <= ~8 GiB each (u32 entry indices stay in range)
-        const uint64_t budget = std::max<uint64_t>(kpb, (8ull << 30) / (4ull * c.k));
+        // passes of <= 5 Gi indices / 4 (C5: 8 passes of 125M keys; measured 35.97-36.19
+        // ms vs 36.50-36.86 with 5 passes of 200M, 36.2-36.5 with 10, 37.4 with 16 and
+        // 36.9-38.2 with 2-3, profiles/r02_ab_c5_passes.txt); u32 entry indices stay in range
+        const uint64_t budget = std::max<uint64_t>(kpb, (5ull << 30) / (4ull * c.k));
         const uint64_t passes = (n + budget - 1) / budget;
         chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, (n + passes - 1) / passes));
         if (const uint64_t v = env_u32("NB_CHUNK_KEYS", 0)) chunk = std::min<uint64_t>(n, v);
