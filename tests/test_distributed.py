@@ -83,9 +83,10 @@ def _partial(kb, ob, key_len, n, m, k, world):
 
 @pytest.mark.parametrize("var,m,k,world", [(True, 1_000_003, 7, 2), (False, 95_851, 10, 2),
                                            (True, 64, 3, 2), (False, 95_851, 7, 3),
-                                           (True, 200_003, 7, 4)])
+                                           (True, 200_003, 7, 4), (False, 95_851, 7, 1)])
 def test_cooperative_or_merge_gloo(tmp_path, oracle, var, m, k, world):
-    """World sizes 2-4 (uneven key shards, word slices that do not divide m)."""
+    """World sizes 2-4 (uneven key shards, word slices that do not divide m), and
+    world size 1 (the partial is returned as the filter, no collective)."""
     from nasp_bloom import distributed as D
     from nasp_bloom import synth
     n = 30_011
