@@ -263,6 +263,12 @@ def valu_frac_of(sq):
     return round(sum(v["valu_floor_us"] for v in ks) / sum(v["avg_duration_us"] for v in ks), 4)
 
 
+def reduce_device(dev):
+    """Where the max-over-ranks timing tensor lives: the GPU for RCCL, the host for
+    the gloo rehearsal (NB_BENCH_BACKEND)."""
+    return dev if os.environ.get("NB_BENCH_BACKEND", "nccl") == "nccl" else "cpu"
+
+
 def kernel_sha():
     import hashlib
     h = hashlib.sha256()
@@ -299,9 +305,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # NB_BENCH_BACKEND=gloo with more ranks than GPUs: a rehearsal of the N > 1 path
+    # on a one-GPU box (ranks share the device; RCCL refuses two ranks per GPU).
+    # The driver's runs use the defaults: RCCL, one rank per GPU.
+    backend = os.environ.get("NB_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     nbm.lib()  # fail loudly if the HIP library is missing
 
@@ -356,7 +371,7 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / args.steps
 
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=reduce_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 
@@ -444,7 +459,7 @@ def bench_merkle(args, world, rank, dev):
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=reduce_device(dev))
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
     B = wl.n * kl + 8 * tsize + 8 * (tsize - 1)
@@ -523,7 +538,7 @@ def bench_cooperative(args, wl, world, rank, dev):
     torch.cuda.synchronize(dev)
     dist.barrier()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=reduce_device(dev))
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t[0])
     value = wl.n * args.steps / elapsed / 1e6
