@@ -717,6 +717,8 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     // (cnt[t] - (A_t << 16)) >> 2 undoes.
     for (uint32_t t = tid; t < T; t += NT) cnt[t] = KR > 0 ? lds_addr(cnt + t) << 16 : 0u;
     if (tid == 0) wave_sums[NT / 64 + 1] = 0u;  // block_any's flag
+    if (STAGE && tid < kLenClasses)  // the staged keys' length-class counters (see below)
+        sorted[(kStageBytes / 4) + 2 * NT + tid] = 0u;
     __syncthreads();
 
     // phase 1: hash each key once; count its k indices per tile.  With KR > 0
@@ -812,19 +814,23 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
                 const uint32_t nvec = (uint32_t)((span + 15) / 16);
                 for (uint32_t q = tid; q < nvec; q += NT) dst[q] = src[q];
             }
-            if (kPermute && staged && tid < kLenClasses) lhist[tid] = 0;
-            __syncthreads();
             uint32_t klo = (uint32_t)(b - kb0 + a0), klen = (uint32_t)(e - b);
             bool kvalid = i < n;
+            // counting sort of the sub-batch by word count (absent keys last): whole
+            // words for the libstdc++ dword path (its loop runs over whole words, then
+            // one tail), all words touched for the byte-wise FNV-1a loop.  The class
+            // counts need only the offsets, so they are taken while the stage copy is
+            // in flight (lhist is zero here: zeroed before the block's first barrier
+            // and again after each permutation is read)
+            uint32_t cls = 0, r = 0;
             if (kPermute && staged) {
-                // counting sort of the sub-batch by word count (absent keys last): whole
-                // words for the libstdc++ dword path (its loop runs over whole words,
-                // then one tail), all words touched for the byte-wise FNV-1a loop
                 const uint32_t nw = FLAVOR == NB_FLAVOR_LIBSTDCXX ? klen >> 3 : (klen + 7) >> 3;
-                const uint32_t cls = kvalid ? min(nw, kLenClasses - 2) : kLenClasses - 1;
+                cls = kvalid ? min(nw, kLenClasses - 2) : kLenClasses - 1;
                 kinfo[tid] = klo | (klen << 16);  // both < 2^16 inside the stage
-                const uint32_t r = atomicAdd(&lhist[cls], 1u);
-                __syncthreads();
+                r = atomicAdd(&lhist[cls], 1u);
+            }
+            __syncthreads();
+            if (kPermute && staged) {
                 if (tid < 64) {
                     const uint32_t cnt = tid < kLenClasses ? lhist[tid] : 0u;
                     const uint32_t st = wave_inclusive_scan(cnt) - cnt;
@@ -838,6 +844,7 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
                 klo = info & 0xffffu;
                 klen = info >> 16;
                 kvalid = pb + src < n;  // == (i < n): the valid keys fill the first slots
+                if (tid < kLenClasses) lhist[tid] = 0u;  // read by all before the barrier above
             }
             if (kvalid) {
                 uint64_t h1, h2;
