@@ -715,6 +715,11 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     // offset within the run.  4 rank <= 4 (2^14 - 1) stays in the low half; a full
     // count of 2^14 carries into the high half, which the decode
     // (cnt[t] - (A_t << 16)) >> 2 undoes.
+    // register-loaded keys: their loads are issued first, in flight across the LDS
+    // initialisation and its barrier
+    const uint64_t base = (uint64_t)blockIdx.x * (KPT * NT);
+    KeyBatch<FLAVOR, LAYOUT, KPT> kb;
+    if (!STAGE) kb.load(keys, offsets, base + tid, NT, n);
     for (uint32_t t = tid; t < T; t += NT) cnt[t] = KR > 0 ? lds_addr(cnt + t) << 16 : 0u;
     if (tid == 0) wave_sums[NT / 64 + 1] = 0u;  // block_any's flag
     if (STAGE && tid < kLenClasses)  // the staged keys' length-class counters (see below)
@@ -729,7 +734,6 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     constexpr int kR = KR > 0 ? KR : 1;
     IndexGen gen[KPT];
     uint32_t ridx[KPT][kR], rank[KPT][kR];
-    const uint64_t base = (uint64_t)blockIdx.x * (KPT * NT);
     auto count_key = [&](int p, uint64_t h1, uint64_t h2) {
         gen[p].start(h1, h2, c);
         IndexGen g = gen[p];
@@ -750,8 +754,6 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
         }
     };
     if (!STAGE) {
-        KeyBatch<FLAVOR, LAYOUT, KPT> kb;
-        kb.load(keys, offsets, base + tid, NT, n);
         // every key of the lane hashed before any count atomic is issued: the
         // compiler otherwise drains key p's LDS atomics (s_waitcnt lgkmcnt(0) at the
         // join of the i < n branch) before it hashes key p + 1
