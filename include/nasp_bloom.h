@@ -70,6 +70,21 @@ int nb_shutdown(void);
 /* Device builds enqueued by this process so far (every build entry point, any
  * device): lets a caller check whether a path reached the GPU. */
 uint64_t nb_device_build_count(void);
+/* The same for device Merkle trees (nb_merkle / nb_merkle_device). */
+uint64_t nb_device_merkle_count(void);
+
+/* Library switches (not part of the filter contract; no switch changes a filter's
+ * bits): the A/B selections between equivalent build paths and the fault
+ * injection the drop-in classes' fallback tests use.  Each is read from the
+ * environment variable of the same name once, on first use; nb_set_knob changes
+ * it for the whole process afterwards (thread-safe).  Names: NB_BUILD_PATH
+ * (0 auto, 1 atomic, 2 tiled), NB_PROBE_PATH (0 auto, 1 one lane per key, 2 tiled),
+ * NB_PACK, NB_TILE_BITS, NB_SHARDS, NB_CHUNK_KEYS, NB_TWO_LEVEL, NB_PACK5,
+ * NB_ENTRY32, NB_RANK, NB_FIXED32, NB_FPMOD, NB_SHARDED_STAGE, NB_FAIL_BUILDS /
+ * NB_FAIL_MERKLES (the next N device builds / trees fail with NB_ERR_HIP).
+ * Unknown names: NB_ERR_ARG. */
+int nb_set_knob(const char *name, uint64_t value);
+int nb_get_knob(const char *name, uint64_t *value);
 
 /* ------------------------------------------------- parameter formulas --- */
 /* BloomFilter::calculateSizeOfBitSet (BloomFilter.cpp:192-194), including the
@@ -78,7 +93,9 @@ uint32_t nb_size_of_bitset(uint32_t n, double p);
 /* BloomFilter::calculateNumberOfHashFunctions (BloomFilter.cpp:196-199). */
 uint32_t nb_num_hashes(uint32_t n, uint32_t m);
 /* std::hash<std::string> of `len` bytes in the selected flavour (host only): the
- * reference's h1 (BloomFilter.cpp:59) and MerkleTree::hash (merkle.cpp:26-32). */
+ * reference's h1 (BloomFilter.cpp:59) and MerkleTree::hash (merkle.cpp:26-32).
+ * NB_FLAVOR_MURMUR3_X64_128 gives the first half of MurmurHash3_x64_128(p, len, 0);
+ * an unknown flavor returns 0 and sets nb_last_error(). */
 uint64_t nb_std_hash(const uint8_t *p, uint64_t len, int flavor);
 /* h2_seed from timeConst: mt19937(timeConst) + uniform_int_distribution<uint64_t>
  * (BloomFilter.cpp:37,44-46). */
@@ -107,12 +124,11 @@ int nb_build_sharded(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
  * batches and for hosts without a usable GPU, e.g. the
  * TypesManager deserialize -> add(one value) -> serialize round trip
  * (System/TypesManager.cpp:74-92).  Same index arithmetic as the kernels
- * (csrc/bloom_math.h); OR-accumulates into host `words`.  Reads key memory in
- * whole aligned 8-byte words that hold key bytes, like the kernels: the buffer
- * must stay addressable up to the aligned word holding its last byte. */
+ * (csrc/bloom_math.h); OR-accumulates into host `words`.  Reads the key bytes only
+ * (no slack or alignment needed). */
 int nb_build_cpu(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                  uint32_t m, uint32_t k, uint64_t h2_seed, int flavor, uint64_t *words);
-/* nb_probe on the calling CPU thread (same key-buffer rule as nb_build_cpu). */
+/* nb_probe on the calling CPU thread (reads the key bytes only). */
 int nb_probe_cpu(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                  uint32_t m, uint32_t k, uint64_t h2_seed, int flavor, const uint64_t *words,
                  uint8_t *out);
@@ -142,7 +158,9 @@ int nb_builder_create(uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
 /* BloomFilter::add of one key (any bytes, len may be 0). */
 int nb_builder_add(nb_builder *b, const uint8_t *key, uint64_t len);
 /* Many keys (same packing as nb_build): uploaded chunk by chunk straight from
- * the caller's buffer, each chunk's build overlapping the next chunk's upload. */
+ * the caller's buffer, each chunk's build overlapping the next chunk's upload.
+ * The caller's buffers may be reused as soon as this returns (every upload from
+ * them has completed); the builds stay asynchronous. */
 int nb_builder_add_batch(nb_builder *b, const uint8_t *keys, const uint64_t *offsets,
                          uint32_t key_len, uint64_t n);
 /* Build everything added so far and copy the filter to `words` (ceil(m/64) host
@@ -199,6 +217,11 @@ int nb_merkle_device(const uint8_t *d_data, const uint64_t *d_offsets, uint32_t 
  * NULL; *root always receives the root hash. */
 int nb_merkle(const uint8_t *data, const uint64_t *offsets, uint32_t rec_len, uint64_t n,
               int flavor, uint64_t *tree, uint64_t *leaves, uint64_t *root, int device);
+/* The same tree on the calling CPU thread (the drop-in MerkleTree's path for small
+ * flushes and hosts without a usable GPU; the kernels' hashing, bloom_math.h).
+ * Reads the record bytes only. */
+int nb_merkle_cpu(const uint8_t *data, const uint64_t *offsets, uint32_t rec_len, uint64_t n,
+                  int flavor, uint64_t *tree, uint64_t *leaves, uint64_t *root);
 
 /* ------------------------------------------------------ serialization --- */
 /* Size of BloomFilter::serialize()'s image: 28 + (uint32_t)(m+7)/8 bytes

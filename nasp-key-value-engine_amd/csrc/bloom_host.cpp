@@ -8,10 +8,13 @@
 //   nb_build_cpu       <- BloomFilter::add (BloomFilter.cpp:82-86) for a small batch on
 //                         the host: the drop-in class's small-batch / no-device path
 //                         (SURVEY §8(b)), with the kernels' own index arithmetic
+//   nb_merkle_cpu      <- MerkleTree(data) (merkle.cpp:7-55) on the host: the drop-in
+//                         MerkleTree's small-flush / no-device path
 #include <cstdint>
 #include <cstring>
 #include <limits>
 #include <random>
+#include <vector>
 
 #include "../../include/nasp_bloom.h"
 #include "bloom_math.h"
@@ -27,6 +30,11 @@ uint64_t nb_seed_from_time(uint32_t time_const) {
 }
 
 uint64_t nb_std_hash(const uint8_t *p, uint64_t len, int flavor) {
+    if (flavor != NB_FLAVOR_LIBSTDCXX && flavor != NB_FLAVOR_MSVC_FNV1A &&
+        flavor != NB_FLAVOR_MURMUR3_X64_128) {
+        (void)nb_internal_fail(NB_ERR_ARG, "nb_std_hash: unknown flavor");
+        return 0;
+    }
     // the kernels' word-stream hash over byte-assembled words (never reads past len)
     auto load = [p, len](uint32_t j) {
         uint64_t w = 0;
@@ -87,8 +95,31 @@ int nb_deserialize(const uint8_t *img, size_t len, uint32_t *m, uint32_t *k, dou
 }  // extern "C"
 
 namespace {
-// The kernels' word-stream hashes of key i on the host: aligned 8-byte words
-// that hold key bytes (never past the key's last aligned word), then the index
+// Aligned word j of a key whose bytes are [lo, hi) (addresses), counted from the
+// aligned word holding byte lo -- the words the kernels' hashes consume -- with
+// the bytes outside the key read as zero (the hashes shift or mask them out), so
+// the host paths read nothing but the caller's key bytes.
+struct KeyWords {
+    uintptr_t base, lo, hi;
+    KeyWords(const uint8_t *p, uint64_t len)
+        : base(reinterpret_cast<uintptr_t>(p) & ~(uintptr_t)7),
+          lo(reinterpret_cast<uintptr_t>(p)), hi(reinterpret_cast<uintptr_t>(p) + len) {}
+    uint32_t a() const { return (uint32_t)(lo - base); }
+    uint64_t operator()(uint32_t j) const {
+        const uintptr_t w = base + 8ull * j;
+        uint64_t r = 0;
+        if (w >= lo && w + 8 <= hi) {
+            std::memcpy(&r, reinterpret_cast<const void *>(w), 8);
+            return r;
+        }
+        for (uint32_t b = 0; b < 8; ++b)
+            if (w + b >= lo && w + b < hi)
+                r |= (uint64_t)*reinterpret_cast<const uint8_t *>(w + b) << (8 * b);
+        return r;
+    }
+};
+
+// The kernels' word-stream hashes of key i on the host, then the index
 // generator -- csrc/bloom_math.h, the code the kernels run.
 template <class F>
 void for_each_key_indices(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
@@ -96,23 +127,17 @@ void for_each_key_indices(const uint8_t *keys, const uint64_t *offsets, uint32_t
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t b = offsets ? offsets[i] : i * (uint64_t)key_len;
         const uint32_t len = (uint32_t)(offsets ? offsets[i + 1] - b : key_len);
-        const uintptr_t addr = reinterpret_cast<uintptr_t>(keys + b);
-        const uint32_t a = (uint32_t)(addr & 7);
-        const uint64_t *q = reinterpret_cast<const uint64_t *>(addr - a);
-        auto load = [q](uint32_t j) {
-            uint64_t w;
-            std::memcpy(&w, q + j, 8);
-            return w;
-        };
+        const KeyWords load(keys + b, len);
+        const uint32_t a = load.a();
         uint64_t h1, h2;
         if (flavor == NB_FLAVOR_MURMUR3_X64_128)
             nb::hash_aligned_words<NB_FLAVOR_MURMUR3_X64_128>(c, load, a, len, &h1, &h2);
         else if (flavor == NB_FLAVOR_MSVC_FNV1A)
             nb::hash_aligned_words<NB_FLAVOR_MSVC_FNV1A>(c, load, a, len, &h1, &h2);
         else if (offsets)
-            nb::hash_aligned_words<NB_FLAVOR_LIBSTDCXX, decltype(load), false>(c, load, a, len, &h1, &h2);
+            nb::hash_aligned_words<NB_FLAVOR_LIBSTDCXX, KeyWords, false>(c, load, a, len, &h1, &h2);
         else
-            nb::hash_aligned_words<NB_FLAVOR_LIBSTDCXX, decltype(load), true>(c, load, a, len, &h1, &h2);
+            nb::hash_aligned_words<NB_FLAVOR_LIBSTDCXX, KeyWords, true>(c, load, a, len, &h1, &h2);
         nb::IndexGen g;
         g.start(h1, h2, c);
         fn(i, g);
@@ -166,6 +191,47 @@ int nb_probe_cpu(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
         }
         out[i] = hit;
     });
+    return NB_OK;
+}
+
+// MerkleTree(data) (merkle.cpp:7-55) on the calling CPU thread, with the Merkle
+// kernels' own hashing (bloom_math.h hash1_aligned_words, hash_dec_pair): the
+// drop-in MerkleTree's path for small flushes and hosts without a usable GPU.
+int nb_merkle_cpu(const uint8_t *data, const uint64_t *offsets, uint32_t rec_len, uint64_t n,
+                  int flavor, uint64_t *tree, uint64_t *leaves, uint64_t *root) {
+    if (n == 0) return nb_internal_fail(NB_ERR_ARG, "MerkleTree of no records (merkle.cpp:8-10 throws)");
+    if (!data || !root) return nb_internal_fail(NB_ERR_ARG, "NULL buffer");
+    if (flavor != NB_FLAVOR_LIBSTDCXX && flavor != NB_FLAVOR_MSVC_FNV1A)
+        return nb_internal_fail(NB_ERR_ARG, "unknown flavor");
+    std::vector<uint64_t> own;
+    uint64_t *t = tree;
+    if (!t) {
+        own.resize(nb_merkle_tree_size(n));
+        t = own.data();
+    }
+    for (uint64_t i = 0; i < n; ++i) {  // leaves: H(record) (merkle.cpp:13-15)
+        const uint64_t b = offsets ? offsets[i] : i * (uint64_t)rec_len;
+        const uint32_t len = (uint32_t)(offsets ? offsets[i + 1] - b : rec_len);
+        const KeyWords load(data + b, len);
+        t[i] = flavor == NB_FLAVOR_MSVC_FNV1A
+                   ? nb::hash1_aligned_words<NB_FLAVOR_MSVC_FNV1A>(load, load.a(), len)
+                   : nb::hash1_aligned_words<NB_FLAVOR_LIBSTDCXX>(load, load.a(), len);
+    }
+    // levels (merkle.cpp:34-55): parent = H(to_string(l) ++ to_string(r)), the last
+    // node of an odd level paired with itself
+    uint64_t in = 0, cnt = n;
+    while (cnt > 1) {
+        const uint64_t out = in + cnt, next = (cnt + 1) / 2;
+        for (uint64_t i = 0; i < next; ++i) {
+            const uint64_t l = t[in + 2 * i], r = 2 * i + 1 < cnt ? t[in + 2 * i + 1] : l;
+            t[out + i] = flavor == NB_FLAVOR_MSVC_FNV1A ? nb::hash_dec_pair<NB_FLAVOR_MSVC_FNV1A>(l, r)
+                                                        : nb::hash_dec_pair<NB_FLAVOR_LIBSTDCXX>(l, r);
+        }
+        in = out;
+        cnt = next;
+    }
+    if (leaves) std::memcpy(leaves, t, n * 8);
+    *root = t[in];
     return NB_OK;
 }
 

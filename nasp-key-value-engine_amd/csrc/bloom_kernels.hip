@@ -28,6 +28,7 @@
 
 #include "../../include/nasp_bloom.h"
 #include "bloom_math.h"
+#include "nb_knobs.h"
 
 using nb::FilterConsts;
 
@@ -1445,10 +1446,7 @@ int ws_reserve(Workspace &w, uint32_t m, size_t bucket_bytes, TileScratch *sc,
 // the super-tile cursors of the two-level build (zero between builds)
 uint32_t *super_cursors(Workspace &w) { return w.zeroed + kCurWords + kMaxTiles; }
 
-uint32_t env_u32(const char *name, uint32_t dflt) {
-    const char *e = std::getenv(name);
-    return e && *e ? (uint32_t)std::strtoul(e, nullptr, 10) : dflt;
-}
+using nb::knob;  // the A/B switches (nb_knobs.h): read once, atomics
 
 // Tile size policy (measured, tools/ubench_tiled.hip): 2^16-bit tiles with 16-bit
 // bucket entries while that needs <= 2048 tiles (m <= 2^27, e.g. C2); smaller
@@ -1464,7 +1462,7 @@ TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     while (ts < 16 && ((uint64_t)m >> (ts + 1)) >= 1024) ++ts;
     while (ts < 20 && (((uint64_t)m + (1ull << ts) - 1) >> ts) > 2048) ++ts;
     auto tiles = [m](uint32_t s) { return ((uint64_t)m + (1ull << s) - 1) >> s; };
-    if (m >= (1u << 24) && k <= 16 && env_u32("NB_PACK", 1) != 0) {
+    if (m >= (1u << 24) && k <= 16 && knob(nb::kKnobPack) != 0) {
         // packed 21-bit entries (k <= 16: the rank-mode tail): larger tiles, down
         // to ~160 of them -- C2 at 2^19-bit tiles (T = 183) 0.162-0.167 ms vs
         // 0.171-0.176 with u16 entries at 2^16 bits (3 interleaved repeats,
@@ -1474,11 +1472,11 @@ TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     } else if (ts > 16) {
         while (ts < 20 && tiles(ts + 1) >= 512) ++ts;
     }
-    ts = std::min<uint32_t>(std::max<uint32_t>(env_u32("NB_TILE_BITS", ts), 12), 20);
+    ts = std::min<uint32_t>(std::max<uint32_t>(knob(nb::kKnobTileBits) ? (uint32_t)knob(nb::kKnobTileBits) : ts, 12), 20);
     tc.ts = ts;
     tc.T = (uint32_t)(((uint64_t)m + (1ull << ts) - 1) >> ts);
     // cursor shards: a power of two (the kernels pick a block's shard with a mask)
-    tc.G = std::min<uint32_t>(std::max<uint32_t>(env_u32("NB_SHARDS", kShards), 1), kShards);
+    tc.G = std::min<uint32_t>(std::max<uint32_t>((uint32_t)std::min<uint64_t>(knob(nb::kKnobShards), kShards), 1), kShards);
     while (tc.G & (tc.G - 1)) tc.G &= tc.G - 1;
     const double e = (double)n_chunk * k / ((double)tc.T * tc.G);
     uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
@@ -1505,19 +1503,14 @@ TileCfg super_tiles(const TileCfg &fine, uint32_t m, uint64_t n_chunk, uint32_t 
 enum class BuildPath { kAuto, kAtomic, kTiled };
 
 BuildPath path_override() {
-    const char *e = std::getenv("NB_BUILD_PATH");
-    if (!e) return BuildPath::kAuto;
-    if (!std::strcmp(e, "atomic")) return BuildPath::kAtomic;
-    if (!std::strcmp(e, "tiled")) return BuildPath::kTiled;
-    return BuildPath::kAuto;
+    const uint64_t v = knob(nb::kKnobBuildPath);
+    return v == 1 ? BuildPath::kAtomic : v == 2 ? BuildPath::kTiled : BuildPath::kAuto;
 }
 
 // Keys per bin/tile pass: the whole batch while its buckets stay under ~8 GB of
 // HBM (one pass over the filter), else equal chunks under that budget.
 uint64_t chunk_keys(uint64_t n, uint32_t k) {
-    const char *e = std::getenv("NB_CHUNK_KEYS");
-    const uint64_t v = e ? std::strtoull(e, nullptr, 10) : 0;
-    if (v) return v;
+    if (const uint64_t v = knob(nb::kKnobChunkKeys)) return v;
     const uint64_t budget = (8ull << 30) / (4ull * std::max<uint32_t>(k, 1));  // keys
     const uint64_t passes = (n + budget - 1) / budget;
     return std::max<uint64_t>(1, (n + passes - 1) / std::max<uint64_t>(passes, 1));
@@ -1590,7 +1583,7 @@ void (*tile_kernel_of())(TileCfg, TileScratch, const void *, uint64_t *, uint64_
 
 // Pass-1 entry type of the two-level build: Pack5 units (k <= 16, the rank-mode
 // tail; NB_PACK5=0 for the A/B) or 32-bit indices.
-bool two_level_pack5() { return env_u32("NB_PACK5", 1) != 0; }
+bool two_level_pack5() { return knob(nb::kKnobPack5) != 0; }
 
 // The two-level build (see bloom_rebin_kernel): per chunk, the bin kernel into
 // super tiles, the re-bin into fine tiles, the tile kernel on the fine tiles.
@@ -1619,7 +1612,7 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
     const uint32_t rebin_x = (uint32_t)(((uint64_t)t1.cap * t1.G + span_units - 1) / span_units);
     // fine entries packed three per word (2^ts2 <= 2^21): capacity in words, the
     // entries' plus <= 2 pad slots per re-bin block of the shard
-    const bool pack = t2.ts <= 20 && env_u32("NB_PACK", 1) != 0;
+    const bool pack = t2.ts <= 20 && knob(nb::kKnobPack) != 0;
     TileCfg t2p = t2;
     if (pack) {
         const uint64_t bps = ((uint64_t)rebin_x + t2.G - 1) / t2.G;
@@ -1674,14 +1667,14 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
     constexpr uint64_t kpb = (uint64_t)KPT * NT;
     uint64_t chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, chunk_keys(n, c.k)));
     TileCfg tc = choose_tiles(c.fm.m, chunk, c.k);
-    if (tc.T > 2 * (uint32_t)NT && env_u32("NB_TWO_LEVEL", 1) != 0) {
+    if (tc.T > 2 * (uint32_t)NT && knob(nb::kKnobTwoLevel) != 0) {
         // passes of <= 5 Gi indices / 4 (C5: 8 passes of 125M keys; measured 35.97-36.19
         // ms vs 36.50-36.86 with 5 passes of 200M, 36.2-36.5 with 10, 37.4 with 16 and
         // 36.9-38.2 with 2-3, profiles/r02_ab_c5_passes.txt); u32 entry indices stay in range
         const uint64_t budget = std::max<uint64_t>(kpb, (5ull << 30) / (4ull * c.k));
         const uint64_t passes = (n + budget - 1) / budget;
         chunk = std::min<uint64_t>(n, std::max<uint64_t>(kpb, (n + passes - 1) / passes));
-        if (const uint64_t v = env_u32("NB_CHUNK_KEYS", 0)) chunk = std::min<uint64_t>(n, v);
+        if (const uint64_t v = knob(nb::kKnobChunkKeys)) chunk = std::min<uint64_t>(n, v);
         tc = choose_tiles(c.fm.m, chunk, c.k);
         if constexpr (KR > 0) {
             if (two_level_pack5())  // 2^(ts+5)-bit super tiles: 25-bit offsets
@@ -1693,7 +1686,7 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
             keys, offsets, key_len, n, c, words, overwrite, st, chunk,
             super_tiles(tc, c.fm.m, chunk, c.k, 6), tc);
     }
-    if (tc.ts <= 16 && env_u32("NB_ENTRY32", 0) == 0)
+    if (tc.ts <= 16 && knob(nb::kKnobEntry32) == 0)
         return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint16_t, NT, STAGE, KR>(
             keys, offsets, key_len, n, c, words, overwrite, st, chunk, tc);
     if constexpr (KR > 0) {
@@ -1708,7 +1701,7 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
         if (STAGE) pk_lds = std::max<size_t>(pk_lds, stage_lds_bytes(NT));
         pk_lds += (size_t)bin_sort_offset_words(tc.T) * 4;
         if (tc.ts <= 20 && tc.T <= 2u * NT && NB_TWO_TILE && pk_lds <= 80 * 1024 &&
-            env_u32("NB_PACK", 1) != 0) {
+            knob(nb::kKnobPack) != 0) {
             const uint64_t nblk = (chunk + kpb - 1) / kpb;
             const uint64_t bps = (nblk + tc.G - 1) / tc.G;
             const uint64_t capw = ((uint64_t)tc.cap + 2 * bps + 2) / 3;
@@ -1732,7 +1725,7 @@ int launch_build_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         // keys per block sized so the block's sorted indices fit in LDS; indices
         // and their in-tile ranks kept in registers while k <= 16 (NB_RANK=0: the
         // regenerate-and-recount variant, kept for A/B)
-        const bool rank = env_u32("NB_RANK", 1) != 0;
+        const bool rank = knob(nb::kKnobRank) != 0;
         if constexpr (vec_layout(LAYOUT)) {
             if (c.k <= 8)
                 return rank ? launch_tiled<FLAVOR, LAYOUT, kBinKPT, kBinThreads, false, 8>(
@@ -1764,7 +1757,7 @@ int launch_build_f(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     if (!offsets && key_len == 16 && (reinterpret_cast<uintptr_t>(keys) & 15) == 0)
         return launch_build_l<FLAVOR, kFixed16>(keys, offsets, key_len, n, c, words, overwrite, st);
     if (!offsets && key_len == 32 && (reinterpret_cast<uintptr_t>(keys) & 15) == 0 &&
-        env_u32("NB_FIXED32", 1) != 0)
+        knob(nb::kKnobFixed32) != 0)
         return launch_build_l<FLAVOR, kFixed32>(keys, offsets, key_len, n, c, words, overwrite, st);
     if (!offsets)
         return launch_build_l<FLAVOR, kFixedStride>(keys, offsets, key_len, n, c, words,
@@ -1802,9 +1795,11 @@ int launch_build(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
         if (overwrite && m) NB_HIP(hipMemsetAsync(words, 0, (((size_t)m + 63) / 64) * 8, st));
         return NB_OK;
     }
+    if (nb::knob_take(nb::kKnobFailBuilds))  // fault injection (drop-in fallback tests)
+        return fail(NB_ERR_HIP, "injected device build failure (NB_FAIL_BUILDS)");
     FilterConsts c = nb::make_consts(m, k, seed, (uint32_t)flavor);
     if (!offsets) nb::set_fixed_len(c, key_len);
-    if (env_u32("NB_FPMOD", 1) == 0) c.fm.fp = 0;  // A/B: integer remainders only
+    if (knob(nb::kKnobFpMod) == 0) c.fm.fp = 0;  // A/B: integer remainders only
     g_device_builds.fetch_add(1, std::memory_order_relaxed);
     if (flavor == NB_FLAVOR_MURMUR3_X64_128)
         return launch_build_f<NB_FLAVOR_MURMUR3_X64_128>(keys, offsets, key_len, n, c, words,
@@ -1826,7 +1821,7 @@ int launch_probe(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
     }
     FilterConsts c = nb::make_consts(m, k, seed, (uint32_t)flavor);
     if (!offsets) nb::set_fixed_len(c, key_len);
-    if (env_u32("NB_FPMOD", 1) == 0) c.fm.fp = 0;
+    if (knob(nb::kKnobFpMod) == 0) c.fm.fp = 0;
     if (flavor == NB_FLAVOR_MURMUR3_X64_128)
         return launch_probe_f<NB_FLAVOR_MURMUR3_X64_128>(keys, offsets, key_len, n, c, words, out, st);
     return flavor == NB_FLAVOR_MSVC_FNV1A

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/nasp_bloom.h"
+#include "nb_knobs.h"
 
 int nb_internal_build(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
                       uint64_t n, uint32_t m, uint32_t k, uint64_t seed, int flavor,
@@ -309,6 +310,9 @@ int nb_builder_add_batch(nb_builder *b, const uint8_t *keys, const uint64_t *off
         i = e;
     }
     b->slot(b->cur).h_offs[0] = 0;
+    // every upload from the caller's buffers has landed: they may be reused (the
+    // builds stay in flight)
+    SB_HIP(hipStreamSynchronize(ss->copy));
     return NB_OK;
 }
 
@@ -395,8 +399,7 @@ int merge_slice(std::vector<nb_builder *> &bs, int o, uint64_t lo, uint64_t len,
     const int dev = own->ss->dev;
     hipStream_t st = own->ss->comp;
     SB_HIP(hipSetDevice(dev));
-    const char *force = std::getenv("NB_SHARDED_STAGE");
-    const bool stage_all = force && *force && *force != '0';
+    const bool stage_all = nb::knob(nb::kKnobShardedStage) != 0;
     std::vector<const uint64_t *> srcs;
     uint64_t *tmp = nullptr;
     size_t staged = 0;

@@ -14,10 +14,12 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 
 #include "../../include/nasp_bloom.h"
 #include "bloom_math.h"
+#include "nb_knobs.h"
 
 int nb_internal_fail(int code, const char *msg);  // bloom_kernels.hip
 
@@ -123,9 +125,13 @@ int launch_merkle(const uint8_t *d_data, const uint64_t *d_offsets, uint32_t rec
     return NB_OK;
 }
 
+std::atomic<uint64_t> g_device_merkles{0};  // nb_device_merkle_count()
+
 }  // namespace
 
 extern "C" {
+
+uint64_t nb_device_merkle_count(void) { return g_device_merkles.load(std::memory_order_relaxed); }
 
 uint64_t nb_merkle_tree_size(uint64_t n) {
     uint64_t total = n;
@@ -142,6 +148,9 @@ int nb_merkle_device(const uint8_t *d_data, const uint64_t *d_offsets, uint32_t 
     if (!d_data || !d_tree) return nb_internal_fail(NB_ERR_ARG, "NULL buffer");
     if (flavor != NB_FLAVOR_LIBSTDCXX && flavor != NB_FLAVOR_MSVC_FNV1A)
         return nb_internal_fail(NB_ERR_ARG, "unknown flavor");
+    if (nb::knob_take(nb::kKnobFailMerkles))  // fault injection (drop-in fallback tests)
+        return nb_internal_fail(NB_ERR_HIP, "injected device Merkle failure (NB_FAIL_MERKLES)");
+    g_device_merkles.fetch_add(1, std::memory_order_relaxed);
     hipStream_t st = (hipStream_t)stream;
     return flavor == NB_FLAVOR_MSVC_FNV1A
                ? launch_merkle<NB_FLAVOR_MSVC_FNV1A>(d_data, d_offsets, rec_len, n, d_tree, st)

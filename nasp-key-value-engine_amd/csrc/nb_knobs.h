@@ -1,0 +1,41 @@
+// nb_knobs.h -- the library's A/B and diagnostic switches.  None of them changes a
+// filter's bits; they select between equivalent build paths (for same-box A/Bs and
+// for the parity tests that pin every path), or inject device failures (for the
+// drop-in classes' fallback tests).
+//
+// The process environment is read once, the first time any knob is consulted
+// (nb_knobs.cpp holds the library's only getenv); afterwards nb_set_knob()
+// (include/nasp_bloom.h) changes a value in place.  Values are atomics, so a
+// build running on another thread sees either the old or the new value, never a
+// torn one -- unlike getenv racing setenv.
+#pragma once
+
+#include <stdint.h>
+
+namespace nb {
+
+enum Knob : int {
+    kKnobBuildPath,     // NB_BUILD_PATH     0 auto | 1 "atomic" | 2 "tiled"
+    kKnobPack,          // NB_PACK           1: packed 21-bit bucket entries (0: 32-bit)
+    kKnobTileBits,      // NB_TILE_BITS      0: tile-size policy, else log2 bits per tile
+    kKnobShards,        // NB_SHARDS         bucket cursor shards (8)
+    kKnobChunkKeys,     // NB_CHUNK_KEYS     0: chunk policy, else keys per bin/tile pass
+    kKnobTwoLevel,      // NB_TWO_LEVEL      1: super tiles + re-bin for T > 2048 tiles
+    kKnobPack5,         // NB_PACK5          1: pass-1 entries five per 16 bytes
+    kKnobEntry32,       // NB_ENTRY32        1: 32-bit entries instead of u16 for small tiles
+    kKnobRank,          // NB_RANK           1: indices + ranks kept in registers (k <= 16)
+    kKnobFixed32,       // NB_FIXED32        1: register path for 16-byte-aligned 32-byte keys
+    kKnobFpMod,         // NB_FPMOD          1: f64-quotient remainders
+    kKnobShardedStage,  // NB_SHARDED_STAGE  1: nb_build_sharded stages every merge source
+    kKnobProbePath,     // NB_PROBE_PATH     0 auto | 1 "lane" (one lane per key) | 2 "tiled"
+    kKnobFailBuilds,    // NB_FAIL_BUILDS    fault injection: the next N device builds fail
+                        //                   with NB_ERR_HIP before launching anything
+    kKnobFailMerkles,   // NB_FAIL_MERKLES   the same for device Merkle trees
+    kKnobCount
+};
+
+uint64_t knob(Knob k);
+// Fault injection: true (and one injected failure consumed) when the knob is > 0.
+bool knob_take(Knob k);
+
+}  // namespace nb

@@ -9,9 +9,15 @@
 //   - a parent is hash(left + right) of the children's decimal strings, the last
 //     node of an odd level paired with itself (merkle.cpp:41-52);
 //   - generateProof / verifyProof walk the levels exactly as merkle.cpp:57-102.
-// What changes inside: the whole tree (every level) is computed on the GPU in one
-// call and kept as the hash values; strings are made when a caller asks for them.
-// A failed device build throws std::runtime_error: there is no CPU fallback.
+// What changes inside: the whole tree (every level) is computed in one call and
+// kept as the hash values; strings are made when a caller asks for them.  A flush
+// of at least hostRecordLimit() records (4 096) is built on the GPU (nb_merkle);
+// a smaller one -- e.g. the reference's tiny-config flushes of two records -- on
+// the host with the Merkle kernels' own hashing (nb_merkle_cpu), with no device
+// call.  If the device build fails (no GPU, a device error) the tree is built on
+// the host after one std::cerr line (once per process when there is no GPU), in
+// the reference's error style (SSTableComp.cpp:543): the constructor throws only
+// what the reference throws (no data).
 #pragma once
 
 // the reference header's includes are kept (its callers rely on them transitively)
@@ -29,6 +35,7 @@ private:
     std::vector<uint64_t> tree;      // every level's hashes, leaves first, root last
     std::vector<uint64_t> level_at;  // first node of each level in `tree`
     std::vector<uint64_t> level_n;   // nodes per level
+    bool on_device = false;          // the tree was built on the GPU
 
     // MerkleTree::hash (merkle.cpp:26-32): decimal string of std::hash<std::string>
     static std::string hash(const std::string &data);
@@ -55,4 +62,8 @@ public:
     // trees written by the authors' Windows build) and device for new trees.
     static void setDefaultFlavor(int flavor);
     static void setDefaultDevice(int device);
+    // Trees of fewer records than this are built on the host (default 4 096).
+    static void setHostRecordLimit(uint64_t records);
+    static uint64_t hostRecordLimit();
+    bool builtOnDevice() const { return on_device; }
 };

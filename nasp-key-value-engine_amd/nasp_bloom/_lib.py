@@ -32,6 +32,9 @@ _SIGS = {
     "nb_last_error": (C.c_char_p, []),
     "nb_shutdown": (C.c_int, []),
     "nb_device_build_count": (C.c_uint64, []),
+    "nb_device_merkle_count": (C.c_uint64, []),
+    "nb_set_knob": (C.c_int, [C.c_char_p, C.c_uint64]),
+    "nb_get_knob": (C.c_int, [C.c_char_p, C.POINTER(C.c_uint64)]),
     "nb_size_of_bitset": (C.c_uint32, [C.c_uint32, C.c_double]),
     "nb_num_hashes": (C.c_uint32, [C.c_uint32, C.c_uint32]),
     "nb_seed_from_time": (C.c_uint64, [C.c_uint32]),
@@ -79,6 +82,8 @@ _SIGS = {
                                    C.c_void_p, C.c_void_p]),
     "nb_merkle": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_int, C.c_void_p,
                             C.c_void_p, C.c_void_p, C.c_int]),
+    "nb_merkle_cpu": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_int, C.c_void_p,
+                                C.c_void_p, C.c_void_p]),
 }
 
 FRAME_RAW = 0

@@ -41,6 +41,46 @@ def std_hash(data: bytes, flavor: int = FLAVOR_LIBSTDCXX) -> int:
     return int(lib().nb_std_hash(data, len(data), flavor))
 
 
+# named values of the path knobs (include/nasp_bloom.h nb_set_knob)
+_KNOB_NAMES = {"NB_BUILD_PATH": {"auto": 0, "atomic": 1, "tiled": 2},
+               "NB_PROBE_PATH": {"auto": 0, "lane": 1, "tiled": 2}}
+
+
+def set_knob(name: str, value) -> None:
+    """nb_set_knob: one of the library's A/B / fault-injection switches, for the
+    whole process (thread-safe; the environment is read only once, at first use)."""
+    if isinstance(value, str):
+        value = _KNOB_NAMES.get(name, {}).get(value, None) if not value.isdigit() else int(value)
+        if value is None:
+            raise NaspBloomError(f"bad value for knob {name}")
+    check(lib().nb_set_knob(name.encode(), int(value)), f"nb_set_knob({name})")
+
+
+def get_knob(name: str) -> int:
+    v = C.c_uint64()
+    check(lib().nb_get_knob(name.encode(), C.byref(v)), f"nb_get_knob({name})")
+    return int(v.value)
+
+
+class knobs:
+    """Context manager: set knobs for a block, restore the previous values after
+    (`with knobs(NB_BUILD_PATH="tiled", NB_CHUNK_KEYS=70000): ...`)."""
+
+    def __init__(self, **kv):
+        self.kv = kv
+        self.saved = {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.saved.setdefault(k, get_knob(k))
+            set_knob(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.saved.items():
+            set_knob(k, v)
+
+
 def _stream_handle(stream) -> int | None:
     if stream is None:
         import torch
@@ -138,6 +178,11 @@ def probe_cpu(keys: np.ndarray, offsets: np.ndarray | None, key_len: int, n: int
 def device_build_count() -> int:
     """Device builds this process has enqueued (nb_device_build_count)."""
     return int(lib().nb_device_build_count())
+
+
+def device_merkle_count() -> int:
+    """Device Merkle trees this process has built (nb_device_merkle_count)."""
+    return int(lib().nb_device_merkle_count())
 
 
 def build_host_sharded(keys: np.ndarray, offsets: np.ndarray | None, key_len: int, n: int, m: int,
@@ -360,9 +405,23 @@ def merkle_host(data: np.ndarray, offsets: np.ndarray | None, rec_len: int, n: i
     return int(root.value), tree
 
 
+def merkle_cpu(data: np.ndarray, offsets: np.ndarray | None, rec_len: int, n: int,
+               flavor: int = FLAVOR_LIBSTDCXX, want_tree: bool = True):
+    """nb_merkle_cpu: the same tree on the calling CPU thread (small flushes, no GPU)."""
+    tree = np.zeros(merkle_tree_size(n), dtype=np.uint64) if want_tree else None
+    root = C.c_uint64()
+    check(lib().nb_merkle_cpu(_np_ptr(data), _np_ptr(offsets), rec_len, n, flavor, _np_ptr(tree),
+                              None, C.addressof(root)), "nb_merkle_cpu")
+    return int(root.value), tree
+
+
 class MerkleTree:
-    """Mirror of the reference MerkleTree (MerkleTree/MerkleTree.h:10-36): the tree is
-    built on the GPU; strings are the decimal hashes the reference stores."""
+    """Mirror of the reference MerkleTree (MerkleTree/MerkleTree.h:10-36): trees of at
+    least HOST_RECORD_LIMIT records are built on the GPU, smaller ones -- and any
+    whose device build fails, after a note on stderr -- on the host with the same
+    hashing (nb_merkle_cpu); strings are the decimal hashes the reference stores."""
+
+    HOST_RECORD_LIMIT = 4096
 
     def __init__(self, data, *, flavor: int = FLAVOR_LIBSTDCXX, device: int = 0):
         recs = [d.encode() if isinstance(d, str) else bytes(d) for d in data]
@@ -371,7 +430,17 @@ class MerkleTree:
         self.flavor = flavor
         buf, offs = _pack(recs)
         self._n = len(recs)
-        _, self._tree = merkle_host(buf, offs, 0, self._n, flavor, device)
+        self.on_device = False
+        if self._n >= self.HOST_RECORD_LIMIT:
+            try:
+                _, self._tree = merkle_host(buf, offs, 0, self._n, flavor, device)
+                self.on_device = True
+            except NaspBloomError as e:  # the reference's error style: report, carry on
+                import sys
+                print(f"[MerkleTree] GPU build failed ({e}); building {self._n} records on the host",
+                      file=sys.stderr)
+        if not self.on_device:
+            _, self._tree = merkle_cpu(buf, offs, 0, self._n, flavor)
         self._levels = []
         at, c = 0, self._n
         while True:

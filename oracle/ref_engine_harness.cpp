@@ -44,6 +44,8 @@ extern "C" time_t time(time_t *out) {
 
 #ifdef NB_ENGINE_DROPIN  // the drop-in build: HIP starts before the clock, as in a running engine
 extern "C" int nb_device_count(void);
+extern "C" unsigned long long nb_device_build_count(void);
+extern "C" unsigned long long nb_device_merkle_count(void);
 #endif
 
 #include "Config.h"
@@ -112,5 +114,9 @@ int main(int argc, char **argv) {
     }
     std::printf("engine done\n");
     std::fprintf(stderr, "engine_ms %.3f\n", ms);
+#ifdef NB_ENGINE_DROPIN  // which flushes reached the GPU (filters, Merkle trees)
+    std::fprintf(stderr, "device_builds %llu device_merkles %llu\n", nb_device_build_count(),
+                 nb_device_merkle_count());
+#endif
     return 0;
 }

@@ -39,3 +39,19 @@ def golden():
     with open(os.path.join(GOLDEN, "msvc_filters.json")) as f:
         msvc = json.load(f)
     return lib, msvc
+
+
+@pytest.fixture
+def knobs(built):
+    """Set library knobs (nb_set_knob) for one test; the previous values come back
+    afterwards.  knobs(NB_BUILD_PATH="tiled", NB_CHUNK_KEYS=70000)."""
+    import nasp_bloom as nbm
+    saved = {}
+
+    def set_(**kv):
+        for k, v in kv.items():
+            saved.setdefault(k, nbm.get_knob(k))
+            nbm.set_knob(k, v)
+    yield set_
+    for k, v in saved.items():
+        nbm.set_knob(k, v)

@@ -15,6 +15,7 @@
 //      one), a TypesManager round trip launches no device build.
 #include <cstdio>
 #include <cstring>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -182,6 +183,93 @@ int main() {
         }
     }
     BloomFilter::setDefaultFlavor(NB_FLAVOR_LIBSTDCXX);
+    // 6. a batch of several chunks (16 MB / 1M keys each): 16-byte keys, then mixed
+    //    lengths from inside the third chunk on -- streamed chunk by chunk to the
+    //    device builder, or (no GPU) built on the host chunk by chunk
+    std::vector<std::string> big;
+    for (uint64_t i = 0; i < 2'600'000; ++i) {
+        char b[40];
+        std::snprintf(b, sizeof b, "%016llx", (unsigned long long)(i * 0x9E3779B97F4A7C15ull));
+        big.emplace_back(b, i < 2'300'000 ? 16 : 1 + i % 29);
+    }
+    {
+        BloomFilter bf((unsigned)big.size(), 0.01);
+        for (auto &x : big) bf.add(x);
+        BloomFilter member;
+        member = bf;
+        auto img = bytes_of(member.serialize());
+        uint32_t m, k, tc; double p; uint64_t seed;
+        header(img, &m, &k, &p, &tc, &seed);
+        EXPECT(img == oracle_image(big, m, k, p, tc, seed, 0), "multi-chunk streamed image");
+        EXPECT(member.lastBuildOnDevice() == gpu, "multi-chunk batch on the GPU iff one is visible");
+        // 7. copies share the words until one side changes: adding to the copy leaves
+        //    the original's image alone (copy on write)
+        BloomFilter copy = member;
+        std::vector<std::string> extra(big.begin(), big.begin() + 10);
+        for (auto &x : extra) x += "-more";
+        for (auto &x : extra) copy.add(x);
+        EXPECT(bytes_of(member.serialize()) == img, "original unchanged after its copy grew");
+        std::vector<std::string> both = big;
+        both.insert(both.end(), extra.begin(), extra.end());
+        EXPECT(bytes_of(copy.serialize()) == oracle_image(both, m, k, p, tc, seed, 0), "copy image");
+        // 8. a moved-from filter is a default one; both can be reused
+        BloomFilter moved = std::move(copy);
+        EXPECT(copy.possiblyContains("anything") && copy.serialize().size() == 28, "moved-from is default");
+        copy = BloomFilter(100, 0.01);
+        copy.add("x");
+        EXPECT(copy.possiblyContains("x"), "moved-from filter reusable");
+        EXPECT(bytes_of(moved.serialize()) == oracle_image(both, m, k, p, tc, seed, 0), "moved-to image");
+        // pending keys move with the object
+        BloomFilter half((unsigned)big.size(), 0.01);
+        for (size_t i = 0; i < 1'500'000; ++i) half.add(big[i]);
+        BloomFilter half2(std::move(half));
+        for (size_t i = 1'500'000; i < big.size(); ++i) half2.add(big[i]);
+        auto himg = bytes_of(half2.serialize());
+        header(himg, &m, &k, &p, &tc, &seed);
+        EXPECT(himg == oracle_image(big, m, k, p, tc, seed, 0), "moved mid-stream image");
+    }
+    // 9. device failures (fault injection, GPU only): a failure while keys stream is
+    //    rebuilt on the host from the retained chunks; past retainBytes() it throws
+    if (gpu) {
+        std::vector<std::string> keys(big.begin(), big.begin() + 50'000);
+        BloomFilter bf((unsigned)keys.size(), 0.01);
+        nb_set_knob("NB_FAIL_BUILDS", 1);
+        for (auto &x : keys) bf.add(x);
+        auto img = bytes_of(bf.serialize());
+        uint32_t m, k, tc; double p; uint64_t seed;
+        header(img, &m, &k, &p, &tc, &seed);
+        EXPECT(img == oracle_image(keys, m, k, p, tc, seed, 0), "injected failure: host rebuild image");
+        EXPECT(!bf.lastBuildOnDevice(), "injected failure: built on the host");
+        // accumulate-after-deserialize with a failure on the second of three chunks
+        BloomFilter base = BloomFilter::deserialize(bf.serialize());
+        for (size_t i = 0; i < 1'200'000; ++i) base.add(big[i]);
+        nb_set_knob("NB_FAIL_BUILDS", 1);  // the chunk handed off next (at 2M keys) fails
+        for (size_t i = 1'200'000; i < big.size(); ++i) base.add(big[i]);
+        std::vector<std::string> all = keys;
+        all.insert(all.end(), big.begin(), big.end());
+        EXPECT(bytes_of(base.serialize()) == oracle_image(all, m, k, p, tc, seed, 0),
+               "mid-stream failure: host rebuild from the deserialized bits");
+        // nothing retained: the failure is reported, not hidden
+        const uint64_t keep = BloomFilter::retainBytes();
+        BloomFilter::setRetainBytes(0);
+        BloomFilter lost((unsigned)big.size(), 0.01);
+        for (size_t i = 0; i < 1'200'000; ++i) lost.add(big[i]);
+        nb_set_knob("NB_FAIL_BUILDS", 1);
+        bool threw = false;
+        try {
+            for (size_t i = 1'200'000; i < big.size(); ++i) lost.add(big[i]);
+            (void)lost.serialize();
+        } catch (const std::runtime_error &e) {
+            threw = std::strstr(e.what(), "injected") != nullptr;
+        }
+        EXPECT(threw, "failure past the retention budget throws with the device error");
+        BloomFilter::setRetainBytes(keep);
+        nb_set_knob("NB_FAIL_BUILDS", 0);
+        BloomFilter again((unsigned)keys.size(), 0.01);
+        for (auto &x : keys) again.add(x);
+        (void)again.serialize();
+        EXPECT(again.lastBuildOnDevice(), "the next filter is built on the device again");
+    }
     nb_shutdown();
     std::printf(failures ? "FAILED %d\n" : "drop-in OK\n", failures);
     return failures ? 1 : 0;

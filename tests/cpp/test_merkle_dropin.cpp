@@ -1,17 +1,23 @@
 // Drop-in MerkleTree test: drives nasp-key-value-engine_amd/host/MerkleTree the way
 // the reference's callers do and checks every string against the oracle
-// (oracle/bloom_oracle.c orc_merkle).  Needs a GPU (the tree is built on it).
+// (oracle/bloom_oracle.c orc_merkle).  Runs with or without a GPU: trees of at
+// least MerkleTree::hostRecordLimit() records are built on the device when one is
+// visible (checked), smaller ones -- and every tree on a GPU-less host -- on the host.
 //   1. the reference's test program (MerkleTree/main.cpp): four records, a proof
 //      for "Podatak2" that verifies;
 //   2. SSTable::build (SSTable/SSTable.cpp:29-42): one value per record, root and
 //      leaves; SSTableRaw's key ++ value records (SSTableRaw.cpp:238);
-//   3. records with NUL bytes and empty records; errors the reference throws.
+//   3. records with NUL bytes and empty records; errors the reference throws;
+//   4. placement: a 2-record flush stays on the host, a 5 000-record one reaches the
+//      GPU (when there is one); an injected device failure (NB_FAIL_MERKLES) is
+//      built on the host with the same strings.
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
+#include "../../include/nasp_bloom.h"
 #include "../../nasp-key-value-engine_amd/host/MerkleTree.h"
 extern "C" {
 #include "../../oracle/bloom_oracle.h"
@@ -117,6 +123,30 @@ int main() {
             threw = true;
         }
         EXPECT(threw, "missing record throws invalid_argument (merkle.cpp:63-65)");
+    }
+    // 4. host / device placement and the device-failure fallback
+    {
+        const bool gpu = nb_device_count() > 0;
+        std::printf("devices: %d\n", nb_device_count());
+        std::vector<std::string> recs;
+        char v[32];
+        for (int i = 0; i < 5000; ++i) {
+            std::snprintf(v, sizeof v, "value-%d", i);
+            recs.push_back(v);
+        }
+        const uint64_t before = nb_device_merkle_count();
+        MerkleTree two(std::vector<std::string>(recs.begin(), recs.begin() + 2));
+        EXPECT(!two.builtOnDevice() && nb_device_merkle_count() == before, "2-record tree on the host");
+        MerkleTree big(recs);
+        EXPECT(big.builtOnDevice() == gpu, "5 000-record tree on the GPU iff one is visible");
+        EXPECT(big.getRootHash() == oracle_tree(recs).root, "5 000-record root");
+        if (gpu) {
+            nb_set_knob("NB_FAIL_MERKLES", 1);
+            MerkleTree fb(recs);
+            EXPECT(!fb.builtOnDevice() && fb.getRootHash() == big.getRootHash() &&
+                       fb.getLeaves() == big.getLeaves(),
+                   "injected device failure: the same tree from the host");
+        }
     }
     if (failures) {
         std::printf("%d failures\n", failures);

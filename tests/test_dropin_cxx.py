@@ -36,7 +36,8 @@ def test_dropin_without_gpu(tmp_path, built):
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=600, env=env)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "devices: 0" in out.stdout and "drop-in OK" in out.stdout
-    assert "[BloomFilter] GPU build failed" in out.stderr
+    assert "[BloomFilter] GPU build failed (no HIP device visible)" in out.stderr
+    assert out.stderr.count("GPU build failed") == 1, "one note per process, not one per filter"
 
 
 @pytest.mark.gpu
@@ -46,4 +47,6 @@ def test_dropin_on_gpu(tmp_path, built):
     assert out.returncode == 0, out.stdout + out.stderr
     assert "devices: 0" not in out.stdout, "the GPU test ran without a device"
     assert "drop-in OK" in out.stdout
-    assert "GPU build failed" not in out.stderr
+    # the only device failures are the injected ones (NB_FAIL_BUILDS, section 9)
+    fails = [l for l in out.stderr.splitlines() if "GPU build failed" in l]
+    assert len(fails) == 2 and all("injected" in l for l in fails), out.stderr

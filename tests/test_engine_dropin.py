@@ -34,10 +34,11 @@ def keys_for(n_tables, n):
     return [b"user%012d" % i for i in idx]
 
 
-def run_engine(exe, d, mode, n, bs, tiered=False, compaction=None, fixed_time=None):
+def run_engine(exe, d, mode, n, bs, tiered=False, compaction=None, fixed_time=None, extra_env=None,
+               want_stderr=False):
     comp = compaction or ("tiered" if tiered else None)
     args = [exe, str(d), mode, str(n), str(bs)] + ([comp] if comp else [])
-    env = dict(os.environ)
+    env = dict(os.environ, **(extra_env or {}))
     if fixed_time is not None:
         env["NB_ENGINE_TIME"] = str(fixed_time)  # the filters' timeConst (harness clock)
     out = subprocess.run(args, capture_output=True, timeout=600, env=env)  # prints raw bytes
@@ -45,7 +46,23 @@ def run_engine(exe, d, mode, n, bs, tiered=False, compaction=None, fixed_time=No
         err = out.stderr[-2000:].decode(errors="replace")
         raise AssertionError(f"{exe} failed rc={out.returncode}: {err}")
     m = re.search(rb"engine_ms ([0-9.]+)", out.stderr)
-    return float(m.group(1)) if m else None
+    ms = float(m.group(1)) if m else None
+    return (ms, out.stderr.decode(errors="replace")) if want_stderr else ms
+
+
+def device_counts(stderr):
+    """(device filter builds, device Merkle trees) the drop-in engine reports."""
+    m = re.search(r"device_builds (\d+) device_merkles (\d+)", stderr)
+    return int(m.group(1)), int(m.group(2))
+
+
+def same_files(d_ref, d_new):
+    files = lambda d: sorted(os.path.relpath(os.path.join(r, f), d) for r, _, fs in os.walk(d)
+                             for f in fs)
+    assert files(d_ref) == files(d_new)
+    for f in files(d_ref):
+        assert open(d_ref / f, "rb").read() == open(d_new / f, "rb").read(), f
+    return files(d_ref)
 
 
 def filter_files(d):
@@ -243,3 +260,48 @@ def test_engine_large_flush_identical_on_gpu(tmp_path, built):
     for f in files(d_ref):
         assert open(d_ref / f, "rb").read() == open(d_new / f, "rb").read(), f
     print(f"\nengine flush of {n} records: reference {ms_ref:.1f} ms, drop-in {ms_new:.1f} ms")
+
+
+# (leveled compaction of raw tables takes the reference engine ~1 min per 3 000
+# records -- its own block I/O -- so leveled runs on the compressed format here)
+@pytest.mark.parametrize("mode,compaction", [("raw", None), ("comp", None), ("raw", "tiered"),
+                                             ("comp", "tiered"), ("comp", "leveled")])
+def test_engine_every_file_identical_without_gpu(tmp_path, mode, compaction, built):
+    """SURVEY §8(b)'s host contract: with no device visible (HIP_VISIBLE_DEVICES
+    empty) the engine on the drop-in BloomFilter and MerkleTree still flushes and
+    compacts, and writes exactly the reference engine's files (filters and Merkle
+    metadata included) -- both classes build on the host with the kernels' own
+    arithmetic, after one note per process on stderr."""
+    if not (os.path.exists(DROPIN_ENGINE) and os.path.exists(REF_ENGINE)):
+        pytest.skip("engine binaries not built (need /root/reference at build time)")
+    n, bs, t = 6000, 4096, 1748963255  # >= 4 096 records: both classes try the device first
+    d_ref, d_new = tmp_path / "ref", tmp_path / "dropin"
+    run_engine(REF_ENGINE, d_ref, mode, n, bs, compaction=compaction, fixed_time=t)
+    _, err = run_engine(DROPIN_ENGINE, d_new, mode, n, bs, compaction=compaction, fixed_time=t,
+                        extra_env={"HIP_VISIBLE_DEVICES": ""}, want_stderr=True)
+    files = same_files(d_ref, d_new)
+    assert len(filter_files(d_ref)) == {None: 1, "tiered": 1, "leveled": 3}[compaction]
+    assert len(files) > 3
+    assert device_counts(err) == (0, 0)
+    assert err.count("[BloomFilter] GPU build failed (no HIP device visible)") == 1
+    assert err.count("[MerkleTree] GPU build failed (no HIP device visible)") == 1
+
+
+@pytest.mark.gpu
+def test_engine_small_flush_stays_on_host(tmp_path, built):
+    """The reference's tiny-config flushes (memtable_max_size 2: two records) launch
+    nothing on the device -- neither a filter build nor a Merkle tree -- and still
+    write the reference's files; a 6 000-record flush reaches the GPU for both."""
+    if not (os.path.exists(DROPIN_ENGINE) and os.path.exists(REF_ENGINE)):
+        pytest.skip("engine binaries not built (need /root/reference at build time)")
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    t = 1748963255
+    for n, want in ((2, (0, 0)), (6000, (1, 1))):
+        d_ref, d_new = tmp_path / f"ref{n}", tmp_path / f"dropin{n}"
+        run_engine(REF_ENGINE, d_ref, "raw", n, 75, fixed_time=t)
+        _, err = run_engine(DROPIN_ENGINE, d_new, "raw", n, 75, fixed_time=t, want_stderr=True)
+        same_files(d_ref, d_new)
+        assert device_counts(err) == want, err
+        assert "GPU build failed" not in err

@@ -111,10 +111,7 @@ def test_merkle_errors(dev):
         nbm.merkle_device(d, None, 4, 2, 7, torch.zeros(3, dtype=torch.int64, device=dev))
 
 
-def test_merkle_dropin_cxx(tmp_path, built):
-    """The C++ drop-in MerkleTree (host/MerkleTree.h) with the reference's usage:
-    the reference's own main.cpp flow, SSTable::build's values, and proofs --
-    every string against the oracle."""
+def build_merkle_dropin(tmp_path):
     exe = tmp_path / "test_merkle_dropin"
     bo = tmp_path / "bo.o"
     subprocess.check_call(["gcc", "-O2", "-c", os.path.join(ORACLE, "bloom_oracle.c"), "-o", str(bo)])
@@ -123,6 +120,17 @@ def test_merkle_dropin_cxx(tmp_path, built):
         "g++", "-O2", "-std=c++17", "-Wall", os.path.join(REPO, "tests", "cpp", "test_merkle_dropin.cpp"),
         os.path.join(PKG, "host", "MerkleTree.cpp"), str(bo), "-L" + libdir, "-lnasp_bloom",
         "-Wl,-rpath," + libdir, "-o", str(exe)])
+    return exe
+
+
+def test_merkle_dropin_cxx(tmp_path, built):
+    """The C++ drop-in MerkleTree (host/MerkleTree.h) with the reference's usage:
+    the reference's own main.cpp flow, SSTable::build's values, and proofs --
+    every string against the oracle; placement (2 records: host, 5 000: GPU) and
+    an injected device failure built on the host."""
+    exe = build_merkle_dropin(tmp_path)
     out = subprocess.run([str(exe)], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout + out.stderr
-    assert "merkle drop-in OK" in out.stdout
+    assert "merkle drop-in OK" in out.stdout and "devices: 0" not in out.stdout
+    fails = [l for l in out.stderr.splitlines() if "GPU build failed" in l]
+    assert len(fails) == 1 and "injected" in fails[0], out.stderr

@@ -29,9 +29,9 @@ def dev(built):
 
 
 @pytest.fixture(params=["auto", "atomic", "tiled"])
-def build_path(request, monkeypatch):
+def build_path(request, knobs):
     """Run a test through each build path of the library (NB_BUILD_PATH)."""
-    monkeypatch.setenv("NB_BUILD_PATH", request.param)
+    knobs(NB_BUILD_PATH=request.param)
     return request.param
 
 
@@ -251,11 +251,9 @@ def test_fixed32_vector_path(dev, oracle, seed, build_path):
         np.testing.assert_array_equal(got, want)
         np.testing.assert_array_equal(oracle.probe(flavor, buf, None, 32, n, m, 10, seed, want),
                                       dev_probe(dev, buf, None, 32, n, m, 10, seed, want, flavor))
-    os.environ["NB_FIXED32"] = "0"
-    try:
+    import nasp_bloom as nbm
+    with nbm.knobs(NB_FIXED32=0):
         got = dev_build(dev, buf, None, 32, n, m, 10, seed)
-    finally:
-        del os.environ["NB_FIXED32"]
     np.testing.assert_array_equal(got, oracle.build(0, buf, None, 32, n, m, 10, seed))
 
 
@@ -341,21 +339,21 @@ def test_device_shape_checks(dev):
 
 
 @pytest.mark.parametrize("k", [1, 8, 9, 16, 17, 24, 32, 33])
-def test_k_range_tiled(dev, oracle, k, monkeypatch):
+def test_k_range_tiled(dev, oracle, k, knobs):
     """k selects the tiled kernel's keys per block (<=8, <=16, <=32) or the atomic path (>32)."""
     from nasp_bloom import synth
-    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    knobs(NB_BUILD_PATH="tiled")
     buf, offs = synth.var_keys(300_000, 4, 40)
     got = dev_build(dev, buf, offs, 0, 300_000, 7_000_003, k, SEED)
     want = oracle.build(0, buf, offs, 0, 300_000, 7_000_003, k, SEED)
     np.testing.assert_array_equal(got, want)
 
 
-def test_tiled_bucket_overflow_spill(dev, oracle, monkeypatch):
+def test_tiled_bucket_overflow_spill(dev, oracle, knobs):
     """Massively duplicated keys overflow the per-tile buckets; the spill path must
     still give the exact filter (SSTable keys are unique, but the API allows this)."""
     from nasp_bloom import synth
-    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    knobs(NB_BUILD_PATH="tiled")
     n = 400_000
     buf = np.zeros(n * 16 + 16, np.uint8)  # 400k identical all-zero 16-byte keys
     buf[: 16 * 1000] = synth.fixed_keys(1000, 16)[: 16 * 1000]  # + 1000 distinct ones
@@ -373,9 +371,9 @@ def test_tiled_bucket_overflow_spill(dev, oracle, monkeypatch):
 # last tiles included.
 @pytest.mark.parametrize("m", [2**27, 2**27 + 1, 2**28 - 1, 300_000_001, 958_505_838,
                                2**30 + 7, 2**31 - 1, 2**31 + 1])
-def test_tile_policy_boundaries(dev, oracle, m, monkeypatch):
+def test_tile_policy_boundaries(dev, oracle, m, knobs):
     from nasp_bloom import synth
-    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    knobs(NB_BUILD_PATH="tiled")
     n = 300_000
     buf = synth.fixed_keys(n, 16)
     got = dev_build(dev, buf, None, 16, n, m, 7, SEED)
@@ -387,7 +385,7 @@ def test_tile_policy_boundaries(dev, oracle, m, monkeypatch):
     np.testing.assert_array_equal(got, want)
 
 
-def test_packed_entries_past_4gib(dev, monkeypatch):
+def test_packed_entries_past_4gib(dev, knobs):
     """Packed bucket words past 4 GiB of buckets (word-indexed write-out): 120M
     keys x k = 16 into m = 900 x 2^20 (900 2^20-bit tiles, packed while two bin
     blocks fit a CU's LDS; 1.92G entries = 5.1 GB of packed words in one chunk) must give the same filter as 32-bit entries
@@ -395,12 +393,12 @@ def test_packed_entries_past_4gib(dev, monkeypatch):
     import torch
     import nasp_bloom as nbm
     from nasp_bloom import synth
-    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    knobs(NB_BUILD_PATH="tiled")
     n, m, k = 120_000_000, 900 << 20, 16
     kt = t_u8(synth.fixed_keys(n, 16), dev)
     out = []
     for pack in ("1", "0"):
-        monkeypatch.setenv("NB_PACK", pack)
+        knobs(NB_PACK=pack)
         wt = torch.zeros(nbm.nwords(m), dtype=torch.int64, device=dev)
         nbm.build_device(kt, None, 16, n, m, k, SEED, 0, wt)
         torch.cuda.synchronize()
@@ -412,10 +410,10 @@ def test_packed_entries_past_4gib(dev, monkeypatch):
     assert int(res.min()) == 1
 
 
-def test_tiled_overflow_spill_large_tiles(dev, oracle, monkeypatch):
+def test_tiled_overflow_spill_large_tiles(dev, oracle, knobs):
     """The spill path with 32-bit entries and 2^20-bit tiles (C4's m)."""
     from nasp_bloom import synth
-    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    knobs(NB_BUILD_PATH="tiled")
     n = 400_000
     buf = np.zeros(n * 16 + 16, np.uint8)
     buf[: 16 * 1000] = synth.fixed_keys(1000, 16)[: 16 * 1000]
@@ -426,15 +424,15 @@ def test_tiled_overflow_spill_large_tiles(dev, oracle, monkeypatch):
 
 @pytest.mark.parametrize("two_level", ["1", "0"])
 @pytest.mark.parametrize("chunk", ["0", "300000"])
-def test_two_level_build_large_m(dev, oracle, two_level, chunk, monkeypatch):
+def test_two_level_build_large_m(dev, oracle, two_level, chunk, knobs):
     """m > 2^31 (C5's 2^32-1): 4 096 fine tiles, built through super tiles + re-bin
     (NB_TWO_LEVEL=1, the default) or binned straight into the fine tiles; chunked
     builds accumulate across chunks; k = 10 and k = 7 (rank paths KR=16 / KR=8)."""
     from nasp_bloom import synth
-    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
-    monkeypatch.setenv("NB_TWO_LEVEL", two_level)
+    knobs(NB_BUILD_PATH="tiled")
+    knobs(NB_TWO_LEVEL=two_level)
     if chunk != "0":
-        monkeypatch.setenv("NB_CHUNK_KEYS", chunk)
+        knobs(NB_CHUNK_KEYS=chunk)
     n = 1_000_003
     buf = synth.fixed_keys(n, 32, seed=77)
     for m, k in ((2**32 - 1, 10), (3_000_000_019, 7)):
@@ -446,11 +444,11 @@ def test_two_level_build_large_m(dev, oracle, two_level, chunk, monkeypatch):
     np.testing.assert_array_equal(got, oracle.build(0, vb, vo, 0, 300_000, 2**32 - 1, 10, SEED))
 
 
-def test_two_level_overflow_spill(dev, oracle, monkeypatch):
+def test_two_level_overflow_spill(dev, oracle, knobs):
     """Duplicated keys overflow both the super-tile and the fine-tile buckets of the
     two-level build: pass 1 spills by fine tile, the re-bin spills too."""
     from nasp_bloom import synth
-    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
+    knobs(NB_BUILD_PATH="tiled")
     n = 400_000
     buf = np.zeros(n * 32 + 16, np.uint8)
     buf[: 32 * 5000] = synth.fixed_keys(5000, 32)[: 32 * 5000]
@@ -460,10 +458,10 @@ def test_two_level_overflow_spill(dev, oracle, monkeypatch):
 
 
 @pytest.mark.parametrize("chunk", ["4096", "100000", "999999"])
-def test_tiled_chunking(dev, oracle, chunk, monkeypatch):
+def test_tiled_chunking(dev, oracle, chunk, knobs):
     from nasp_bloom import synth
-    monkeypatch.setenv("NB_BUILD_PATH", "tiled")
-    monkeypatch.setenv("NB_CHUNK_KEYS", chunk)
+    knobs(NB_BUILD_PATH="tiled")
+    knobs(NB_CHUNK_KEYS=chunk)
     buf, offs = synth.var_keys(1_000_000)
     got = dev_build(dev, buf, offs, 0, 1_000_000, 9_585_059, 7, SEED)
     want = oracle.build(0, buf, offs, 0, 1_000_000, 9_585_059, 7, SEED)
@@ -474,13 +472,13 @@ def test_tiled_chunking(dev, oracle, chunk, monkeypatch):
 
 
 @pytest.mark.parametrize("path", ["atomic", "tiled"])
-def test_overwrite_mode(dev, oracle, path, monkeypatch):
+def test_overwrite_mode(dev, oracle, path, knobs):
     """NB_BUILD_OVERWRITE: the words become the batch's filter whatever they held
     before -- including when buckets spill (duplicated keys) and across chunks."""
     import torch
     import nasp_bloom as nbm
     from nasp_bloom import synth
-    monkeypatch.setenv("NB_BUILD_PATH", path)
+    knobs(NB_BUILD_PATH=path)
     m, k = 9_585_059, 7
     buf, offs = synth.var_keys(500_000)
     kt, ot = t_u8(buf, dev), t_u64(offs, dev)
@@ -493,7 +491,7 @@ def test_overwrite_mode(dev, oracle, path, monkeypatch):
     dup = np.zeros(300_000 * 16 + 16, np.uint8)
     dup[:16 * 500] = synth.fixed_keys(500, 16)[:16 * 500]
     stale.fill_(-1)
-    monkeypatch.setenv("NB_CHUNK_KEYS", "70000")
+    knobs(NB_CHUNK_KEYS="70000")
     nbm.build_device(t_u8(dup, dev), None, 16, 300_000, m, k, SEED, 0, stale, overwrite=True)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(stale.cpu().numpy().view(np.uint64),

@@ -73,12 +73,12 @@ def test_sharded_accumulates_and_edges(nbm, oracle):
 
 
 @pytest.mark.parametrize("nshards", [2, 3, 8])
-def test_sharded_forced_staging(nbm, oracle, monkeypatch, nshards):
+def test_sharded_forced_staging(nbm, oracle, knobs, nshards):
     """NB_SHARDED_STAGE=1: every source of the slice merge goes through the
     blocking hipMemcpyPeer staging branch (taken for real only between devices
     without peer access), bit-exact against the oracle, both key layouts."""
     from nasp_bloom import synth
-    monkeypatch.setenv("NB_SHARDED_STAGE", "1")
+    knobs(NB_SHARDED_STAGE=1)
     n = 300_007
     buf, offs = synth.var_keys(n)
     m, k = 2_875_519, 7
