@@ -168,6 +168,12 @@ int nb_builder_add_batch(nb_builder *b, const uint8_t *keys, const uint64_t *off
 int nb_builder_finish(nb_builder *b, uint64_t *words);
 int nb_builder_destroy(nb_builder *b);
 
+/* Page-locked host memory for key chunks handed to a builder (their uploads are
+ * then true asynchronous DMA): the drop-in class packs keys straight into such
+ * chunks.  NB_ERR_NODEV without a device (use ordinary memory then). */
+int nb_host_alloc(size_t bytes, void **out);
+int nb_host_free(void *p);
+
 /* ------------------------------------------ device-resident entry points --- */
 /* Same contracts; every pointer is device memory on the current device and
  * the work is enqueued on `stream` (a hipStream_t; NULL = the null stream).

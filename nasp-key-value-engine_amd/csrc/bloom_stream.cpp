@@ -164,6 +164,21 @@ struct nb_builder {
 
 extern "C" {
 
+int nb_host_alloc(size_t bytes, void **out) {
+    if (!out) return nb_internal_fail(NB_ERR_ARG, "NULL out");
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        return nb_internal_fail(NB_ERR_NODEV, "no HIP device visible");
+    SB_HIP(hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+    return NB_OK;
+}
+
+int nb_host_free(void *p) {
+    if (p) SB_HIP(hipHostFree(p));
+    return NB_OK;
+}
+
 int nb_builder_create(uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
                       const uint64_t *init_words, int device, nb_builder **out) {
     if (!out) return nb_internal_fail(NB_ERR_ARG, "NULL out");

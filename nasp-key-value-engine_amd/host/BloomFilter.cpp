@@ -24,34 +24,44 @@ constexpr uint64_t kChunkBytes = uint64_t(16) << 20;  // key bytes per chunk
 constexpr uint64_t kChunkKeys = uint64_t(1) << 20;    // keys per chunk
 constexpr uint64_t kSlack = 16;
 
-// Process-wide pool of chunk buffers: a flush that streams 10M keys reuses the
-// buffers (and their already-faulted pages) of the previous flush.
+// Process-wide pools of chunk buffers: a flush that streams 10M keys reuses the
+// buffers (pinned by nb_host_alloc, so their uploads are asynchronous DMA; plain
+// memory on a host without a device) of the previous flush.  Key buffers and
+// offset buffers (needed only once a chunk's key lengths differ) pool separately.
+struct Buf {
+    void *p;
+    bool pinned;
+};
 std::mutex g_pool_mu;
-std::vector<std::pair<uint8_t *, uint64_t *>> g_pool;
-constexpr size_t kPoolMax = 24;
+std::vector<Buf> g_pool[2];  // [0] key bytes, [1] offsets
+constexpr size_t kPoolMax = 20;
+constexpr size_t kBufBytes[2] = {kChunkBytes + kSlack, (kChunkKeys + 1) * 8};
 
-std::pair<uint8_t *, uint64_t *> pool_get() {
+Buf pool_get(int which) {
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
-        if (!g_pool.empty()) {
-            auto b = g_pool.back();
-            g_pool.pop_back();
+        if (!g_pool[which].empty()) {
+            const Buf b = g_pool[which].back();
+            g_pool[which].pop_back();
             return b;
         }
     }
-    return {new uint8_t[kChunkBytes + kSlack], new uint64_t[kChunkKeys + 1]};
+    void *p = nullptr;
+    if (nb_host_alloc(kBufBytes[which], &p) == NB_OK) return {p, true};
+    return {::operator new(kBufBytes[which]), false};
 }
 
-void pool_put(uint8_t *bytes, uint64_t *offs) {
+void pool_put(int which, void *p, bool pinned) {
+    if (!p) return;
     {
         std::lock_guard<std::mutex> lk(g_pool_mu);
-        if (g_pool.size() < kPoolMax) {
-            g_pool.emplace_back(bytes, offs);
+        if (g_pool[which].size() < kPoolMax) {
+            g_pool[which].push_back({p, pinned});
             return;
         }
     }
-    delete[] bytes;
-    delete[] offs;
+    if (pinned) (void)nb_host_free(p);
+    else ::operator delete(p);
 }
 }  // namespace
 
@@ -163,13 +173,23 @@ void BloomFilter::release_chunks() const {
 }
 
 void BloomFilter::free_chunk(Chunk &c) {
-    if (c.key_cap == kChunkKeys) pool_put(c.bytes, c.offs);
-    else {
+    if (c.key_cap == kChunkKeys) {
+        pool_put(0, c.bytes, c.pinned);
+        pool_put(1, c.offs, c.offs_pinned);
+    } else {  // an oversized key's own chunk
         delete[] c.bytes;
         delete[] c.offs;
     }
     c.bytes = nullptr;
     c.offs = nullptr;
+}
+
+// The chunk's offsets array (n + 1 entries), allocated on first need.
+void BloomFilter::need_offsets(Chunk &c) {
+    if (c.offs) return;
+    const Buf b = pool_get(1);
+    c.offs = static_cast<uint64_t *>(b.p);
+    c.offs_pinned = b.pinned;
 }
 
 // The words, allocated and owned by this filter alone (copy on write).
@@ -190,7 +210,9 @@ void BloomFilter::add(const std::string &elem) {
         if (!pending.empty()) hand_off();
         Chunk c;
         if (len <= kChunkBytes) {
-            std::tie(c.bytes, c.offs) = pool_get();
+            const Buf b = pool_get(0);
+            c.bytes = static_cast<uint8_t *>(b.p);
+            c.pinned = b.pinned;
             c.byte_cap = kChunkBytes;
             c.key_cap = kChunkKeys;
         } else {  // one oversized key: a chunk of its own
@@ -199,13 +221,13 @@ void BloomFilter::add(const std::string &elem) {
             c.byte_cap = len;
             c.key_cap = 1;
         }
-        c.offs[0] = 0;
         pending.push_back(c);
     }
     Chunk &c = pending.back();
     if (c.fixed == -1) {
         c.fixed = (int64_t)len;
     } else if (c.fixed >= 0 && c.fixed != (int64_t)len) {  // lengths differ from here on
+        need_offsets(c);
         for (uint64_t i = 0; i <= c.n; ++i) c.offs[i] = i * (uint64_t)c.fixed;
         c.fixed = -2;
     }
@@ -244,19 +266,23 @@ void BloomFilter::open_device() const {
     mode = Mode::kHost;
 }
 
-bool BloomFilter::stream_chunk(const Chunk &c) const {
+bool BloomFilter::stream_chunk(Chunk &c) const {
     if (c.fixed > 0) return nb_builder_add_batch(stream, c.bytes, nullptr, (uint32_t)c.fixed, c.n) == NB_OK;
-    if (c.fixed == 0)
-        for (uint64_t i = 0; i <= c.n; ++i) c.offs[i] = 0;  // all keys empty
+    if (c.fixed == 0) {  // all keys empty
+        need_offsets(c);
+        for (uint64_t i = 0; i <= c.n; ++i) c.offs[i] = 0;
+    }
     return nb_builder_add_batch(stream, c.bytes, c.offs, 0, c.n) == NB_OK;
 }
 
 // The pending batch through nb_build_cpu (the kernels' index arithmetic) into the
 // filter's own words.
-void BloomFilter::build_chunk_on_host(const Chunk &c) const {
+void BloomFilter::build_chunk_on_host(Chunk &c) const {
     std::vector<uint64_t> &w = own_bits();
-    if (c.fixed == 0)
+    if (c.fixed == 0) {
+        need_offsets(c);
         for (uint64_t i = 0; i <= c.n; ++i) c.offs[i] = 0;
+    }
     const int rc = c.fixed > 0 ? nb_build_cpu(c.bytes, nullptr, (uint32_t)c.fixed, c.n, m, k, h2_seed,
                                               flavor, w.data())
                                : nb_build_cpu(c.bytes, c.offs, 0, c.n, m, k, h2_seed, flavor, w.data());

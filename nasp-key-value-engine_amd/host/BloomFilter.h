@@ -12,7 +12,8 @@
 //     copies until one of them changes (`bloom_ = bf`, SSTable.cpp:35, copies no
 //     bits);
 //   - add() packs the key into a host chunk (16 MB of key bytes / 1M keys; offsets
-//     only once the chunk's key lengths differ).  Once the keys added since the
+//     only once the chunk's key lengths differ; page-locked via nb_host_alloc and
+//     pooled across filters, so a chunk's upload is an asynchronous DMA).  Once the keys added since the
 //     last read reach hostBatchLimit() (4 096, the library's own host/device
 //     cut-over) a streaming device builder (nb_builder_*) is opened, and from then
 //     on every chunk that fills is handed to it at once: its upload and device
@@ -71,8 +72,9 @@ private:
 
     // A host chunk of packed keys (buffers come from a process-wide pool).
     struct Chunk {
-        uint8_t *bytes = nullptr;    // kChunkBytes capacity
-        uint64_t *offs = nullptr;    // kChunkKeys + 1 entries, used once lengths differ
+        uint8_t *bytes = nullptr;    // kChunkBytes capacity (pinned when a device is visible)
+        uint64_t *offs = nullptr;    // kChunkKeys + 1 entries, allocated once lengths differ
+        bool pinned = false, offs_pinned = false;
         uint64_t used = 0, n = 0;    // key bytes, keys
         uint64_t byte_cap = 0, key_cap = 0;  // kChunkBytes / kChunkKeys (pooled), or
                                              // one oversized key's exact size
@@ -92,12 +94,13 @@ private:
     void flush() const;
     void hand_off() const;                   // the chunks in `pending` leave it
     void open_device() const;                // kPending -> kDevice (or kHost)
-    bool stream_chunk(const Chunk &c) const; // false: the device failed
+    bool stream_chunk(Chunk &c) const;       // false: the device failed
     void device_failed(const char *what) const;
-    void build_chunk_on_host(const Chunk &c) const;
+    void build_chunk_on_host(Chunk &c) const;
     std::vector<uint64_t> &own_bits() const; // unshared, allocated words
     void release_chunks() const;
     static void free_chunk(Chunk &c);
+    static void need_offsets(Chunk &c);
     void reset_moved() noexcept;
 
 public:

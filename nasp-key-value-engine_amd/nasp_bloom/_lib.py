@@ -77,6 +77,8 @@ _SIGS = {
                                        C.c_uint64]),
     "nb_builder_finish": (C.c_int, [C.c_void_p, C.c_void_p]),
     "nb_builder_destroy": (C.c_int, [C.c_void_p]),
+    "nb_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(C.c_void_p)]),
+    "nb_host_free": (C.c_int, [C.c_void_p]),
     "nb_merkle_tree_size": (C.c_uint64, [C.c_uint64]),
     "nb_merkle_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_int,
                                    C.c_void_p, C.c_void_p]),

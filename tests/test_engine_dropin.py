@@ -291,14 +291,16 @@ def test_engine_every_file_identical_without_gpu(tmp_path, mode, compaction, bui
 def test_engine_small_flush_stays_on_host(tmp_path, built):
     """The reference's tiny-config flushes (memtable_max_size 2: two records) launch
     nothing on the device -- neither a filter build nor a Merkle tree -- and still
-    write the reference's files; a 6 000-record flush reaches the GPU for both."""
+    write the reference's files; a 6 000-record flush reaches the GPU for both (one
+    filter; two Merkle trees: SSTable::build's over the values and SSTableRaw's over
+    key ++ value records, SSTableRaw.cpp:238,392-402)."""
     if not (os.path.exists(DROPIN_ENGINE) and os.path.exists(REF_ENGINE)):
         pytest.skip("engine binaries not built (need /root/reference at build time)")
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     t = 1748963255
-    for n, want in ((2, (0, 0)), (6000, (1, 1))):
+    for n, want in ((2, (0, 0)), (6000, (1, 2))):
         d_ref, d_new = tmp_path / f"ref{n}", tmp_path / f"dropin{n}"
         run_engine(REF_ENGINE, d_ref, "raw", n, 75, fixed_time=t)
         _, err = run_engine(DROPIN_ENGINE, d_new, "raw", n, 75, fixed_time=t, want_stderr=True)
