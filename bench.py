@@ -205,9 +205,12 @@ def c2_rate(nbm, synth, dev, stream, flavor, steps=20):
 
 def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=5):
     """Batch possiblyContains (nb_probe_device, BloomFilter.cpp:67-80) over the filter
-    just built: the batch's own keys (every one present: k gathers each) and as many
-    absent keys (early exit at the first zero bit; their positive rate is the
-    filter's measured false-positive rate).  Reported beside `value`."""
+    just built: the batch's own keys (every one present) and as many absent keys
+    (their positive rate is the filter's measured false-positive rate), on each
+    probe path (NB_PROBE_PATH): `auto` (the library's default: a sampled prefix picks
+    the path on the device), `lane` (one lane per key, k gathers with early exit) and
+    `tiled` (lookups binned by filter tile and tested in LDS).  Reported beside
+    `value`."""
     import torch
     import nasp_bloom as nbm
     from nasp_bloom import synth
@@ -216,22 +219,27 @@ def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=
     a_o = torch.from_numpy(a_offs.view(np.int64)).to(dev) if a_offs is not None else None
     out_t = torch.empty(wl.n, dtype=torch.uint8, device=dev)
     res = {}
-    for name, kk, oo in (("present", keys, offs), ("absent", absent, a_o)):
-        with torch.cuda.stream(stream):
-            nbm.probe_device(kk, oo, key_len, wl.n, wl.m, wl.k, seed, flavor, words, out_t,
-                             stream=stream)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            with torch.cuda.stream(stream):
-                nbm.probe_device(kk, oo, key_len, wl.n, wl.m, wl.k, seed, flavor, words, out_t,
-                                 stream=stream)
-        e1.record(stream)
-        torch.cuda.synchronize(dev)
-        ms = e0.elapsed_time(e1) / reps
-        res[name] = {"value": round(wl.n / (ms * 1e-3) / 1e6, 3), "unit": "Mkeys/s", "ms": round(ms, 4),
-                     "positive_rate": round(float(out_t.float().mean()), 6)}
-    res["note"] = "one lane per key, k gathers with early exit; absent keys from another seed"
+    for path in ("auto", "lane", "tiled"):
+        r = {}
+        with nbm.knobs(NB_PROBE_PATH=path):
+            for name, kk, oo in (("present", keys, offs), ("absent", absent, a_o)):
+                with torch.cuda.stream(stream):
+                    nbm.probe_device(kk, oo, key_len, wl.n, wl.m, wl.k, seed, flavor, words, out_t,
+                                     stream=stream)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(reps):
+                    with torch.cuda.stream(stream):
+                        nbm.probe_device(kk, oo, key_len, wl.n, wl.m, wl.k, seed, flavor, words, out_t,
+                                         stream=stream)
+                e1.record(stream)
+                torch.cuda.synchronize(dev)
+                ms = e0.elapsed_time(e1) / reps
+                r[name] = {"value": round(wl.n / (ms * 1e-3) / 1e6, 3), "unit": "Mkeys/s",
+                           "ms": round(ms, 4), "positive_rate": round(float(out_t.float().mean()), 6)}
+        res[path] = r
+    res["note"] = ("auto = the default (lane kernel on a 64k-key sample, its hit rate picks lane "
+                   "or tiled for the rest); absent keys from another seed")
     return res
 
 

@@ -243,11 +243,33 @@ __global__ __launch_bounds__(kBlock) void bloom_build_atomic_kernel(
     }
 }
 
+// The probe's auto mode (launch_probe_tiled): the lane kernel probes a sample of
+// the batch first and counts its positives; every later kernel reads that count and
+// runs only if its path is the one chosen (a block-uniform early exit), so the
+// choice needs no host synchronisation and the launch sequence stays
+// graph-capturable.
+struct ProbeGate {
+    uint32_t *hits;          // sample launch: add its positives here (nullptr: none)
+    const uint32_t *decide;  // nullptr: always run; else run iff the choice == want
+    uint32_t sample;         // keys in the sample
+    uint32_t want;           // 1 the lane path, 2 the tiled path
+};
+__device__ __forceinline__ bool gate_open(const ProbeGate &g) {
+    if (!g.decide) return true;
+    // tiled when at least half the sample was present
+    const uint32_t choice = 2ull * *g.decide >= g.sample ? 2u : 1u;
+    return choice == g.want;
+}
+
+// One lane per key, k gathers with an early exit at the first zero bit.
 template <int FLAVOR, int LAYOUT>
 __global__ __launch_bounds__(kBlock) void bloom_probe_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
-    uint64_t n, FilterConsts c, const uint32_t *__restrict__ words32, uint8_t *__restrict__ out) {
+    uint64_t n, FilterConsts c, const uint32_t *__restrict__ words32, uint8_t *__restrict__ out,
+    ProbeGate gate) {
+    if (!gate_open(gate)) return;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint32_t hits = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
         uint64_t h1, h2;
         hashes_of<FLAVOR, LAYOUT>(c, keys, offsets, key_len, i, &h1, &h2);
@@ -259,6 +281,11 @@ __global__ __launch_bounds__(kBlock) void bloom_probe_kernel(
             if (!((words32[g.r >> 5] >> (g.r & 31)) & 1u)) { hit = 0; break; }
         }
         out[i] = hit;
+        hits += hit;
+    }
+    if (gate.hits) {  // one atomic per wave
+        for (int o = 32; o; o >>= 1) hits += __shfl_xor(hits, o);
+        if ((threadIdx.x & 63) == 0 && hits) atomicAdd(gate.hits, hits);
     }
 }
 
@@ -690,6 +717,195 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     }
 }
 
+// Phase 1 of the bin kernels (the build's bloom_bin_kernel and the tiled probe's
+// probe_bin_kernel): initialise the block's tile counters, hash its KPT * NT keys
+// once and count every index per tile with an LDS atomic.  In rank mode (KR > 0,
+// k <= KR) the count atomic's return value is the index's placement handle, and
+// index + handle stay in registers for the placement; otherwise only the index
+// generator's start state (6 registers per key) is kept and the placement
+// regenerates the indices.  kid[p]: the key (index in the launch) slot p of this
+// lane hashed -- staged variable-length keys are hashed in a permuted order.
+template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR>
+struct BinPhase1 {
+    static constexpr int kR = KR > 0 ? KR : 1;
+    IndexGen gen[KPT];
+    uint32_t ridx[KPT][kR], rank[KPT][kR];
+    uint64_t kid[KPT];
+
+    __device__ __forceinline__ void run(const uint8_t *__restrict__ keys,
+                                        const uint64_t *__restrict__ offsets, uint32_t key_len,
+                                        uint64_t n, const FilterConsts &c, uint32_t ts, uint32_t T,
+                                        uint32_t *cnt, uint32_t *sorted, uint32_t *any_flag,
+                                        uint64_t base) {
+        const uint32_t tid = threadIdx.x;
+        KeyBatch<FLAVOR, LAYOUT, KPT> kb;
+        if (!STAGE) kb.load(keys, offsets, base + tid, NT, n);
+        for (uint32_t t = tid; t < T; t += NT) cnt[t] = KR > 0 ? lds_addr(cnt + t) << 16 : 0u;
+        if (tid == 0) *any_flag = 0u;  // block_any's flag
+        if (STAGE && tid < kLenClasses)  // the staged keys' length-class counters (see below)
+            sorted[(kStageBytes / 4) + 2 * NT + tid] = 0u;
+        __syncthreads();
+
+        // phase 1: hash each key once; count its k indices per tile.  With KR > 0
+        // (k <= KR) the count atomic's return value is the index's rank in its tile's
+        // block-local run, and index + rank stay in registers for phase 3; otherwise
+        // only the index generator's start state (6 registers per key) is kept and
+        // phase 3 regenerates the indices.
+        auto count_key = [&](int p, uint64_t h1, uint64_t h2) {
+            gen[p].start(h1, h2, c);
+            IndexGen g = gen[p];
+            if (KR > 0) {
+#pragma unroll
+                for (int j = 0; j < kR; ++j) {
+                    if (j < (int)c.k) {
+                        if (j) g.next(c);
+                        ridx[p][j] = g.r;
+                        rank[p][j] = NB_DIAG_NOCOUNT ? g.r : atomicAdd(&cnt[g.r >> ts], 4u);
+                    }
+                }
+            } else {
+                for (uint32_t j = 0; j < c.k; ++j) {
+                    if (j) g.next(c);
+                    atomicAdd(&cnt[g.r >> ts], 1u);
+                }
+            }
+        };
+        if (!STAGE) {
+            // every key of the lane hashed before any count atomic is issued: the
+            // compiler otherwise drains key p's LDS atomics (s_waitcnt lgkmcnt(0) at the
+            // join of the i < n branch) before it hashes key p + 1
+            uint64_t h1[KPT], h2[KPT];
+#pragma unroll
+            for (int p = 0; p < KPT; ++p)  // (a lane past n hashes its stale registers)
+                kb.hash(c, keys, key_len, base + (uint64_t)p * NT + tid, p, &h1[p], &h2[p]);
+#pragma unroll
+            for (int p = 0; p < KPT; ++p)
+                if (base + (uint64_t)p * NT + tid < n) count_key(p, h1[p], h2[p]);
+#pragma unroll
+            for (int p = 0; p < KPT; ++p) kid[p] = base + (uint64_t)p * NT + tid;
+        } else {
+            // Variable-length (or odd fixed-length) keys, one sub-batch of NT keys at a
+            // time: its keys are one contiguous byte range.  When that fits the stage
+            // (the not-yet-used sort array) it is loaded into LDS with coalesced 16-byte
+            // loads and every key is hashed from LDS; otherwise (very long keys) the
+            // lanes read HBM.
+            uint8_t *stage = reinterpret_cast<uint8_t *>(sorted);
+            auto koff = [&](uint64_t i) -> uint64_t {
+                return LAYOUT == kOffsets ? offsets[i] : i * (uint64_t)key_len;
+            };
+            // libstdc++ start states per key length (h1: lsx_init, h2: after the seed's
+            // whole prefix words), tabulated once per block after the stage's key-info,
+            // permutation and class arrays; the first sub-batch's barrier publishes them
+            uint64_t *init_tab = reinterpret_cast<uint64_t *>(
+                stage + kStageBytes + (2 * (size_t)NT + kLenClasses) * 4);  // [2][kInitLens]
+            if (FLAVOR == NB_FLAVOR_LIBSTDCXX && tid < kInitLens) {
+                init_tab[tid] = nb::lsx_init(tid);
+                init_tab[kInitLens + tid] =
+                    LAYOUT == kFixedStride ? c.h2_init_fixed : nb::lsx_h2_start(c, tid);
+            }
+#pragma unroll
+            for (int p = 0; p < KPT; ++p) {
+                const uint64_t pb = base + (uint64_t)p * NT;  // first key of the sub-batch
+                if (pb >= n) break;                           // block-uniform
+                const uint64_t pe = min(pb + NT, n);
+                const uint64_t i = pb + tid;
+                uint64_t b = 0, e = 0;
+                if (i < n) {
+                    b = koff(i);
+                    e = koff(i + 1);
+                }
+                // the stage copy starts at the 16-byte-aligned address at or below the
+                // sub-batch's first key byte: every vector it loads then holds a byte of
+                // the caller's key range (or shares its 16-byte granule), so no load
+                // crosses into an unmapped page, however the key buffer is aligned
+                const uint64_t kb0 = koff(pb);
+                const uint32_t a0 = (uint32_t)((reinterpret_cast<uintptr_t>(keys) + kb0) & 15u);
+                const uint64_t span = koff(pe) - kb0 + a0;
+                const bool staged = span <= (uint64_t)kStageBytes;  // block-uniform
+                // staged variable-length keys are hashed in order of their word count: a
+                // wave's lanes then loop over like lengths instead of its longest key
+                constexpr bool kPermute = LAYOUT == kOffsets;
+                uint32_t *kinfo = reinterpret_cast<uint32_t *>(stage + kStageBytes);  // [NT]
+                uint32_t *perm = kinfo + NT;                                         // [NT]
+                uint32_t *lhist = perm + NT;                                         // [kLenClasses]
+                if (p) __syncthreads();  // the previous sub-batch is hashed: the stage is free
+                if (staged) {
+                    const uint4 *src = reinterpret_cast<const uint4 *>(keys + kb0 - a0);
+                    uint4 *dst = reinterpret_cast<uint4 *>(stage);
+                    const uint32_t nvec = (uint32_t)((span + 15) / 16);
+                    for (uint32_t q = tid; q < nvec; q += NT) dst[q] = src[q];
+                }
+                uint32_t klo = (uint32_t)(b - kb0 + a0), klen = (uint32_t)(e - b);
+                kid[p] = i;
+                bool kvalid = i < n;
+                // counting sort of the sub-batch by word count (absent keys last): whole
+                // words for the libstdc++ dword path (its loop runs over whole words, then
+                // one tail), all words touched for the byte-wise FNV-1a loop.  The class
+                // counts need only the offsets, so they are taken while the stage copy is
+                // in flight (lhist is zero here: zeroed before the block's first barrier
+                // and again after each permutation is read)
+                uint32_t cls = 0, r = 0;
+                if (kPermute && staged) {
+                    const uint32_t nw = FLAVOR == NB_FLAVOR_LIBSTDCXX ? klen >> 3 : (klen + 7) >> 3;
+                    cls = kvalid ? min(nw, kLenClasses - 2) : kLenClasses - 1;
+                    kinfo[tid] = klo | (klen << 16);  // both < 2^16 inside the stage
+                    r = atomicAdd(&lhist[cls], 1u);
+                }
+                __syncthreads();
+                if (kPermute && staged) {
+                    if (tid < 64) {
+                        const uint32_t cnt = tid < kLenClasses ? lhist[tid] : 0u;
+                        const uint32_t st = wave_inclusive_scan(cnt) - cnt;
+                        if (tid < kLenClasses) lhist[tid] = st;
+                    }
+                    __syncthreads();
+                    perm[lhist[cls] + r] = tid;
+                    __syncthreads();
+                    const uint32_t src = perm[tid];  // a key of this sub-batch; valid ones first
+                    const uint32_t info = kinfo[src];
+                    klo = info & 0xffffu;
+                    klen = info >> 16;
+                    kvalid = pb + src < n;  // == (i < n): the valid keys fill the first slots
+                    kid[p] = pb + src;
+                    if (tid < kLenClasses) lhist[tid] = 0u;  // read by all before the barrier above
+                }
+                if (kvalid) {
+                    uint64_t h1, h2;
+                    const uint32_t len = klen;
+                    if (staged && FLAVOR == NB_FLAVOR_LIBSTDCXX) {
+                        // dword stream from LDS (bloom_math.h lsx_hash_dwords); its reads run
+                        // <= 12 bytes past the key, inside the stage's allocation
+                        const uint32_t *dw = reinterpret_cast<const uint32_t *>(stage) + (klo >> 2);
+                        auto D = [dw](uint32_t j) { return dw[j]; };
+                        const uint32_t sh = 8 * (klo & 3u);
+                        uint64_t h0, g0;
+                        if (len < kInitLens) {
+                            h0 = init_tab[len];
+                            g0 = init_tab[kInitLens + len];
+                        } else {
+                            h0 = nb::lsx_init(len);
+                            g0 = LAYOUT == kFixedStride ? c.h2_init_fixed : nb::lsx_h2_start(c, len);
+                        }
+                        if (c.prem == 0) nb::lsx_hash_dwords<0>(c, D, sh, len, h0, g0, &h1, &h2);
+                        else if (c.prem <= 4) nb::lsx_hash_dwords<1>(c, D, sh, len, h0, g0, &h1, &h2);
+                        else nb::lsx_hash_dwords<2>(c, D, sh, len, h0, g0, &h1, &h2);
+                    } else if (staged) {
+                        const uint32_t lo = klo, a = lo & 7u;
+                        const uint64_t *q = reinterpret_cast<const uint64_t *>(stage + (lo - a));
+                        auto load = [q](uint32_t j) { return q[j]; };
+                        nb::hash_aligned_words<FLAVOR, decltype(load), LAYOUT == kFixedStride>(
+                            c, load, a, len, &h1, &h2);
+                    } else {
+                        key_hashes_ptr<FLAVOR, LAYOUT == kFixedStride>(c, keys + b, len, &h1, &h2);
+                    }
+                    count_key(p, h1, h2);
+                }
+            }
+        }
+        __syncthreads();
+    }
+};
+
 // Two resident blocks per CU (8 waves per SIMD at NT = 1024): <= 64 VGPRs.
 #ifndef NB_BIN_MIN_WAVES
 #define NB_BIN_MIN_WAVES(NT) (2 * (NT) / 256)
@@ -719,170 +935,12 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     // register-loaded keys: their loads are issued first, in flight across the LDS
     // initialisation and its barrier
     const uint64_t base = (uint64_t)blockIdx.x * (KPT * NT);
-    KeyBatch<FLAVOR, LAYOUT, KPT> kb;
-    if (!STAGE) kb.load(keys, offsets, base + tid, NT, n);
-    for (uint32_t t = tid; t < T; t += NT) cnt[t] = KR > 0 ? lds_addr(cnt + t) << 16 : 0u;
-    if (tid == 0) wave_sums[NT / 64 + 1] = 0u;  // block_any's flag
-    if (STAGE && tid < kLenClasses)  // the staged keys' length-class counters (see below)
-        sorted[(kStageBytes / 4) + 2 * NT + tid] = 0u;
-    __syncthreads();
-
-    // phase 1: hash each key once; count its k indices per tile.  With KR > 0
-    // (k <= KR) the count atomic's return value is the index's rank in its tile's
-    // block-local run, and index + rank stay in registers for phase 3; otherwise
-    // only the index generator's start state (6 registers per key) is kept and
-    // phase 3 regenerates the indices.
     constexpr int kR = KR > 0 ? KR : 1;
-    IndexGen gen[KPT];
-    uint32_t ridx[KPT][kR], rank[KPT][kR];
-    auto count_key = [&](int p, uint64_t h1, uint64_t h2) {
-        gen[p].start(h1, h2, c);
-        IndexGen g = gen[p];
-        if (KR > 0) {
-#pragma unroll
-            for (int j = 0; j < kR; ++j) {
-                if (j < (int)c.k) {
-                    if (j) g.next(c);
-                    ridx[p][j] = g.r;
-                    rank[p][j] = NB_DIAG_NOCOUNT ? g.r : atomicAdd(&cnt[g.r >> tc.ts], 4u);
-                }
-            }
-        } else {
-            for (uint32_t j = 0; j < c.k; ++j) {
-                if (j) g.next(c);
-                atomicAdd(&cnt[g.r >> tc.ts], 1u);
-            }
-        }
-    };
-    if (!STAGE) {
-        // every key of the lane hashed before any count atomic is issued: the
-        // compiler otherwise drains key p's LDS atomics (s_waitcnt lgkmcnt(0) at the
-        // join of the i < n branch) before it hashes key p + 1
-        uint64_t h1[KPT], h2[KPT];
-#pragma unroll
-        for (int p = 0; p < KPT; ++p)  // (a lane past n hashes its stale registers)
-            kb.hash(c, keys, key_len, base + (uint64_t)p * NT + tid, p, &h1[p], &h2[p]);
-#pragma unroll
-        for (int p = 0; p < KPT; ++p)
-            if (base + (uint64_t)p * NT + tid < n) count_key(p, h1[p], h2[p]);
-    } else {
-        // Variable-length (or odd fixed-length) keys, one sub-batch of NT keys at a
-        // time: its keys are one contiguous byte range.  When that fits the stage
-        // (the not-yet-used sort array) it is loaded into LDS with coalesced 16-byte
-        // loads and every key is hashed from LDS; otherwise (very long keys) the
-        // lanes read HBM.
-        uint8_t *stage = reinterpret_cast<uint8_t *>(sorted);
-        auto koff = [&](uint64_t i) -> uint64_t {
-            return LAYOUT == kOffsets ? offsets[i] : i * (uint64_t)key_len;
-        };
-        // libstdc++ start states per key length (h1: lsx_init, h2: after the seed's
-        // whole prefix words), tabulated once per block after the stage's key-info,
-        // permutation and class arrays; the first sub-batch's barrier publishes them
-        uint64_t *init_tab = reinterpret_cast<uint64_t *>(
-            stage + kStageBytes + (2 * (size_t)NT + kLenClasses) * 4);  // [2][kInitLens]
-        if (FLAVOR == NB_FLAVOR_LIBSTDCXX && tid < kInitLens) {
-            init_tab[tid] = nb::lsx_init(tid);
-            init_tab[kInitLens + tid] =
-                LAYOUT == kFixedStride ? c.h2_init_fixed : nb::lsx_h2_start(c, tid);
-        }
-#pragma unroll
-        for (int p = 0; p < KPT; ++p) {
-            const uint64_t pb = base + (uint64_t)p * NT;  // first key of the sub-batch
-            if (pb >= n) break;                           // block-uniform
-            const uint64_t pe = min(pb + NT, n);
-            const uint64_t i = pb + tid;
-            uint64_t b = 0, e = 0;
-            if (i < n) {
-                b = koff(i);
-                e = koff(i + 1);
-            }
-            // the stage copy starts at the 16-byte-aligned address at or below the
-            // sub-batch's first key byte: every vector it loads then holds a byte of
-            // the caller's key range (or shares its 16-byte granule), so no load
-            // crosses into an unmapped page, however the key buffer is aligned
-            const uint64_t kb0 = koff(pb);
-            const uint32_t a0 = (uint32_t)((reinterpret_cast<uintptr_t>(keys) + kb0) & 15u);
-            const uint64_t span = koff(pe) - kb0 + a0;
-            const bool staged = span <= (uint64_t)kStageBytes;  // block-uniform
-            // staged variable-length keys are hashed in order of their word count: a
-            // wave's lanes then loop over like lengths instead of its longest key
-            constexpr bool kPermute = LAYOUT == kOffsets;
-            uint32_t *kinfo = reinterpret_cast<uint32_t *>(stage + kStageBytes);  // [NT]
-            uint32_t *perm = kinfo + NT;                                         // [NT]
-            uint32_t *lhist = perm + NT;                                         // [kLenClasses]
-            if (p) __syncthreads();  // the previous sub-batch is hashed: the stage is free
-            if (staged) {
-                const uint4 *src = reinterpret_cast<const uint4 *>(keys + kb0 - a0);
-                uint4 *dst = reinterpret_cast<uint4 *>(stage);
-                const uint32_t nvec = (uint32_t)((span + 15) / 16);
-                for (uint32_t q = tid; q < nvec; q += NT) dst[q] = src[q];
-            }
-            uint32_t klo = (uint32_t)(b - kb0 + a0), klen = (uint32_t)(e - b);
-            bool kvalid = i < n;
-            // counting sort of the sub-batch by word count (absent keys last): whole
-            // words for the libstdc++ dword path (its loop runs over whole words, then
-            // one tail), all words touched for the byte-wise FNV-1a loop.  The class
-            // counts need only the offsets, so they are taken while the stage copy is
-            // in flight (lhist is zero here: zeroed before the block's first barrier
-            // and again after each permutation is read)
-            uint32_t cls = 0, r = 0;
-            if (kPermute && staged) {
-                const uint32_t nw = FLAVOR == NB_FLAVOR_LIBSTDCXX ? klen >> 3 : (klen + 7) >> 3;
-                cls = kvalid ? min(nw, kLenClasses - 2) : kLenClasses - 1;
-                kinfo[tid] = klo | (klen << 16);  // both < 2^16 inside the stage
-                r = atomicAdd(&lhist[cls], 1u);
-            }
-            __syncthreads();
-            if (kPermute && staged) {
-                if (tid < 64) {
-                    const uint32_t cnt = tid < kLenClasses ? lhist[tid] : 0u;
-                    const uint32_t st = wave_inclusive_scan(cnt) - cnt;
-                    if (tid < kLenClasses) lhist[tid] = st;
-                }
-                __syncthreads();
-                perm[lhist[cls] + r] = tid;
-                __syncthreads();
-                const uint32_t src = perm[tid];  // a key of this sub-batch; valid ones first
-                const uint32_t info = kinfo[src];
-                klo = info & 0xffffu;
-                klen = info >> 16;
-                kvalid = pb + src < n;  // == (i < n): the valid keys fill the first slots
-                if (tid < kLenClasses) lhist[tid] = 0u;  // read by all before the barrier above
-            }
-            if (kvalid) {
-                uint64_t h1, h2;
-                const uint32_t len = klen;
-                if (staged && FLAVOR == NB_FLAVOR_LIBSTDCXX) {
-                    // dword stream from LDS (bloom_math.h lsx_hash_dwords); its reads run
-                    // <= 12 bytes past the key, inside the stage's allocation
-                    const uint32_t *dw = reinterpret_cast<const uint32_t *>(stage) + (klo >> 2);
-                    auto D = [dw](uint32_t j) { return dw[j]; };
-                    const uint32_t sh = 8 * (klo & 3u);
-                    uint64_t h0, g0;
-                    if (len < kInitLens) {
-                        h0 = init_tab[len];
-                        g0 = init_tab[kInitLens + len];
-                    } else {
-                        h0 = nb::lsx_init(len);
-                        g0 = LAYOUT == kFixedStride ? c.h2_init_fixed : nb::lsx_h2_start(c, len);
-                    }
-                    if (c.prem == 0) nb::lsx_hash_dwords<0>(c, D, sh, len, h0, g0, &h1, &h2);
-                    else if (c.prem <= 4) nb::lsx_hash_dwords<1>(c, D, sh, len, h0, g0, &h1, &h2);
-                    else nb::lsx_hash_dwords<2>(c, D, sh, len, h0, g0, &h1, &h2);
-                } else if (staged) {
-                    const uint32_t lo = klo, a = lo & 7u;
-                    const uint64_t *q = reinterpret_cast<const uint64_t *>(stage + (lo - a));
-                    auto load = [q](uint32_t j) { return q[j]; };
-                    nb::hash_aligned_words<FLAVOR, decltype(load), LAYOUT == kFixedStride>(
-                        c, load, a, len, &h1, &h2);
-                } else {
-                    key_hashes_ptr<FLAVOR, LAYOUT == kFixedStride>(c, keys + b, len, &h1, &h2);
-                }
-                count_key(p, h1, h2);
-            }
-        }
-    }
-    __syncthreads();
+    BinPhase1<FLAVOR, LAYOUT, KPT, NT, STAGE, KR> ph;
+    ph.run(keys, offsets, key_len, n, c, tc.ts, T, cnt, sorted, wave_sums + NT / 64 + 1, base);
+    IndexGen (&gen)[KPT] = ph.gen;
+    const uint32_t (&ridx)[KPT][kR] = ph.ridx;
+    const uint32_t (&rank)[KPT][kR] = ph.rank;
     if (NB_DIAG_STOP(1)) return;
     if constexpr (pack_of<ENTRY>() > 1) {  // packed entries (host-checked T <= 2 NT, KR > 0)
         bin_tail_two_tiles<NT, KPT, kR>(lds, bin_sort_offset_words(T), tc, sc, buckets, base, n,
@@ -1303,6 +1361,138 @@ __global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
     }
 }
 
+// ------------------------------------------------------------ tiled probe ----
+// The batch form of possiblyContains (BloomFilter.cpp:67-80) for large, mostly
+// present batches.  One lane per key gathers k random words of the filter (~56 G
+// gathers/s chip-wide for a 114 MiB filter: 12.5 ms for C4's 100M present keys);
+// binned like the build, the same lookups become streaming traffic:
+//   probe_bin_kernel : phase 1 of the build's bin kernel (hash, count per tile),
+//                      then every index is written to its tile's bucket as a 64-bit
+//                      entry (key << 32 | in-tile offset) -- no packing, no pads;
+//                      each key's answer starts at 1;
+//   probe_tile_kernel: one block per tile: the tile's filter words into LDS, then
+//                      every entry tests its bit there; a zero bit stores 0 into the
+//                      key's answer byte (plain byte stores: every writer writes the
+//                      same value).
+// Present keys cost no stores at all; an absent key costs one store per zero bit
+// (~k/2), which is why absent-heavy batches keep the lane path (ProbeGate).
+constexpr int kProbeThreads = 1024;
+
+__host__ __device__ constexpr uint32_t probe_sort_offset_words(uint32_t T) {
+    return (4 * T + 32 + 3) & ~3u;  // cnt | S | GX | L | wave_sums, 16-byte aligned
+}
+
+template <int FLAVOR, int LAYOUT, bool STAGE, int KR>
+__global__ __launch_bounds__(kProbeThreads, 2) void probe_bin_kernel(
+    const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
+    uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc, uint64_t *__restrict__ buckets,
+    const uint64_t *__restrict__ words, uint8_t *__restrict__ out, ProbeGate gate) {
+    constexpr int NT = kProbeThreads;
+    if (!gate_open(gate)) return;
+    extern __shared__ uint32_t lds[];
+    const uint32_t T = tc.T, tid = threadIdx.x, k = c.k;
+    uint32_t *cnt = lds, *S = lds + T, *GX = lds + 2 * T, *L = lds + 3 * T;
+    uint32_t *wave_sums = lds + 4 * T;  // [NT/64 + 2]
+    uint32_t *sidx = lds + probe_sort_offset_words(T);  // [NT * k] indices, sorted by tile
+    uint32_t *skid = sidx + NT * k;                     // [NT * k] their keys
+    const uint64_t base = (uint64_t)blockIdx.x * NT;
+    BinPhase1<FLAVOR, LAYOUT, 1, NT, STAGE, KR> ph;
+    ph.run(keys, offsets, key_len, n, c, tc.ts, T, cnt, sidx, wave_sums + NT / 64 + 1, base);
+    const bool valid = base + tid < n;  // (staged keys: the valid ones fill the first slots)
+    if (valid) out[ph.kid[0]] = 1;
+    // counts from the placement handles (A_t << 16 | 4 rank, see BinPhase1)
+    for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << 16)) >> 2;
+    __syncthreads();
+    const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
+    // reserve a run in every touched tile's bucket shard; GX[t] = its first entry
+    // minus the run's local start, L[t] = the first local position past capacity
+    const uint32_t shard = blockIdx.x & (tc.G - 1);
+    uint32_t *cur = sc.gcur + (size_t)shard * T;
+    for (uint32_t t = tid; t < T; t += NT) {
+        const uint32_t h = cnt[t], g = h ? atomicAdd(&cur[t], h) : 0u;
+        GX[t] = (t * tc.G + shard) * tc.cap + g - S[t];
+        L[t] = S[t] + (g < tc.cap ? tc.cap - g : 0u);
+    }
+    // placement (the reservations' round trips overlap it)
+    if (valid) {
+#pragma unroll
+        for (int j = 0; j < KR; ++j)
+            if (j < (int)k) {
+                const uint32_t pos = S[ph.ridx[0][j] >> tc.ts] + ((ph.rank[0][j] & 0xffffu) >> 2);
+                sidx[pos] = ph.ridx[0][j];
+                skid[pos] = (uint32_t)ph.kid[0];
+            }
+    }
+    __syncthreads();
+    // write-out: one 64-bit entry per index, runs contiguous; an entry past its
+    // bucket's capacity (pathological duplicates only) is tested right here
+    const uint32_t msk = (1u << tc.ts) - 1;
+    for (uint32_t q = tid; q < total; q += NT) {
+        const uint32_t v = sidx[q], t = v >> tc.ts, kq = skid[q];
+        if (q < L[t]) {
+            buckets[(uint32_t)(GX[t] + q)] = ((uint64_t)kq << 32) | (v & msk);
+        } else if (!((words[v >> 6] >> (v & 63)) & 1u)) {
+            out[kq] = 0;
+        }
+    }
+}
+
+template <int NT = kTileThreads>
+__global__ __launch_bounds__(NT) void probe_tile_kernel(TileCfg tc, TileScratch sc,
+                                                        const uint64_t *__restrict__ buckets,
+                                                        const uint64_t *__restrict__ words,
+                                                        uint64_t nwords, uint8_t *__restrict__ out,
+                                                        ProbeGate gate) {
+    if (!gate_open(gate)) return;
+    extern __shared__ uint32_t tile[];  // [2^ts / 32] filter words, then 2*kShards+1 words
+    const uint32_t t = blockIdx.x, tid = threadIdx.x;
+    const uint32_t tile_words32 = 1u << (tc.ts - 5), mask = (1u << tc.ts) - 1;
+    uint32_t *shard_cnt = tile + tile_words32;  // [kShards]
+    uint32_t *shard_v0 = shard_cnt + kShards;   // [kShards + 1]
+    // the tile's filter words (past the filter's end: zero, never tested)
+    const uint64_t w0 = (uint64_t)t << (tc.ts - 6);
+    uint64_t *tile64 = reinterpret_cast<uint64_t *>(tile);
+    for (uint32_t w = tid; w < tile_words32 / 2; w += NT)
+        tile64[w] = w0 + w < nwords ? words[w0 + w] : 0ull;
+    if (tid < tc.G) {
+        uint32_t *cp = sc.gcur + (size_t)tid * tc.T + t;
+        shard_cnt[tid] = min(*cp, tc.cap);
+        *cp = 0;  // workspace invariant: cursors are zero between launches
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t v0 = 0;
+        for (uint32_t g = 0; g < tc.G; ++g) {
+            shard_v0[g] = v0;
+            v0 += shard_cnt[g];
+        }
+        shard_v0[tc.G] = v0;
+    }
+    __syncthreads();
+    const uint64_t *tb = buckets + (size_t)t * tc.G * tc.cap;
+    const uint32_t ne = shard_v0[tc.G];
+    auto test = [&](uint64_t e) {
+        const uint32_t off = (uint32_t)e & mask;
+        if (!((tile[off >> 5] >> (off & 31)) & 1u)) out[(uint32_t)(e >> 32)] = 0;
+    };
+    // the G shards as one flat range of entries; a lane's entry indices only grow,
+    // so its shard index is advanced, never searched
+    uint32_t g = 0;
+    auto entry_at = [&](uint32_t q) {
+        while (g + 1 < tc.G && q >= shard_v0[g + 1]) ++g;
+        return tb[(size_t)g * tc.cap + (q - shard_v0[g])];
+    };
+    uint32_t q = tid;
+    for (; q + 3 * NT < ne; q += 4 * NT) {
+        uint64_t e[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) e[u] = entry_at(q + u * NT);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) test(e[u]);
+    }
+    for (; q < ne; q += NT) test(entry_at(q));
+}
+
 __global__ __launch_bounds__(kBlock) void or_merge_kernel(uint64_t *__restrict__ dst,
                                                           const uint64_t *__restrict__ src,
                                                           uint64_t nwords, uint32_t nsrc,
@@ -1379,6 +1569,7 @@ struct Workspace {
     size_t bucket_bytes = 0;
     void *buckets2 = nullptr;     // fine buckets of the two-level build
     size_t bucket2_bytes = 0;
+    uint32_t *probe_hits = nullptr;  // the auto probe's sample count (ProbeGate)
 };
 std::mutex g_ws_mu;
 std::vector<Workspace *> g_ws;
@@ -1765,25 +1956,135 @@ int launch_build_f(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     return launch_build_l<FLAVOR, kOffsets>(keys, offsets, key_len, n, c, words, overwrite, st);
 }
 
+// Probe tiles: the largest 2^ts <= 2^20 (the tile kernel's LDS copy) that still
+// leaves >= 256 tiles; cap per (tile, shard) as the build's.
+TileCfg probe_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
+    TileCfg tc;
+    uint32_t ts = 12;
+    while (ts < 20 && (((uint64_t)m + (1ull << (ts + 1)) - 1) >> (ts + 1)) >= 256) ++ts;
+    tc.ts = ts;
+    tc.T = (uint32_t)(((uint64_t)m + (1ull << ts) - 1) >> ts);
+    tc.G = kShards;
+    const double e = (double)n_chunk * k / ((double)tc.T * tc.G);
+    uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
+    tc.cap = (uint32_t)std::min<uint64_t>((cap + 7) & ~7ull, 0xFFFFFFC0ull);
+    tc.fts = ts;
+    return tc;
+}
+
+// Auto mode's sample (the first kProbeSample keys, probed by the lane kernel) and
+// the smallest batch the tiled path is considered for.
+constexpr uint64_t kProbeSample = 1 << 16;
+constexpr uint64_t kProbeTiledMin = 1 << 22;
+
+template <int FLAVOR, int LAYOUT>
+int launch_probe_lane(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                      const FilterConsts &c, const uint64_t *words, uint8_t *out, hipStream_t st,
+                      const ProbeGate &gate) {
+    hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, LAYOUT>), dim3(grid_for(n)), dim3(kBlock), 0, st,
+                       keys, offsets, key_len, n, c, reinterpret_cast<const uint32_t *>(words), out,
+                       gate);
+    NB_HIP(hipGetLastError());
+    return NB_OK;
+}
+
+template <int FLAVOR, int LAYOUT, int KR>
+int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                       const FilterConsts &c, const uint64_t *words, uint8_t *out, hipStream_t st,
+                       const ProbeGate &gate) {
+    constexpr bool STAGE = !vec_layout(LAYOUT);
+    constexpr int NT = kProbeThreads;
+    Workspace *ws;
+    TileScratch sc;
+    int rc;
+    if ((rc = get_ws(st, &ws))) return rc;
+    std::lock_guard<std::mutex> lk(ws->mu);
+    // chunks whose 64-bit entries stay under ~6 GB of buckets (key ids < 2^32)
+    const uint64_t budget = std::max<uint64_t>(NT, (6ull << 30) / (10ull * c.k));
+    const uint64_t passes = (n + budget - 1) / budget;
+    const uint64_t chunk = std::max<uint64_t>(1, (n + passes - 1) / passes);
+    const TileCfg tc = probe_tiles(c.fm.m, chunk, c.k);
+    if ((rc = ws_reserve(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * 8, &sc))) return rc;
+    size_t sort_bytes = (size_t)2 * NT * c.k * 4;
+    if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(NT));
+    const size_t bin_lds = (size_t)probe_sort_offset_words(tc.T) * 4 + sort_bytes;
+    const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
+    auto bin = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR>;
+    auto tile = probe_tile_kernel<kTileThreads>;
+    if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(tile, tile_lds))) return rc;
+    const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
+    uint64_t *bk = reinterpret_cast<uint64_t *>(ws->buckets);
+    for (uint64_t done = 0; done < n; done += chunk) {
+        const uint64_t cn = std::min(chunk, n - done);
+        const uint8_t *ck = offsets ? keys : keys + done * key_len;
+        const uint64_t *co = offsets ? offsets + done : nullptr;
+        hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + NT - 1) / NT)), dim3(NT), bin_lds, st, ck, co,
+                           key_len, cn, c, tc, sc, bk, words, out + done, gate);
+        NB_HIP(hipGetLastError());
+        hipLaunchKernelGGL(tile, dim3(tc.T), dim3(kTileThreads), tile_lds, st, tc, sc,
+                           (const uint64_t *)bk, words, nwords, out + done, gate);
+        NB_HIP(hipGetLastError());
+    }
+    return NB_OK;
+}
+
+// The path of a batch probe (NB_PROBE_PATH: 0 auto, 1 lane, 2 tiled): lane for small
+// batches, k > 8 (k > 16 for 32-byte keys) and the non-parity MurmurHash3 flavour;
+// auto probes a sample with the lane kernel first and lets its hit rate pick the
+// path for the rest (ProbeGate), without a host round trip.
+template <int FLAVOR, int LAYOUT>
+int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
+                   const FilterConsts &c, const uint64_t *words, uint8_t *out, hipStream_t st) {
+    const uint64_t path = knob(nb::kKnobProbePath);
+    constexpr bool kTiledLayout = LAYOUT != kFixedStride && FLAVOR != NB_FLAVOR_MURMUR3_X64_128;
+    const uint32_t kmax = LAYOUT == kFixed32 ? 16u : 8u;
+    const bool tiled_ok = kTiledLayout && c.k <= kmax &&
+                          probe_tiles(c.fm.m, n, c.k).T <= kMaxTiles;
+    const ProbeGate none{nullptr, nullptr, 0, 0};
+    if (path == 1 || !tiled_ok || (path == 0 && n < kProbeTiledMin))
+        return launch_probe_lane<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, out, st, none);
+    auto tiled = [&](const uint8_t *k_, const uint64_t *o_, uint64_t n_, uint8_t *out_,
+                     const ProbeGate &g) -> int {
+        if constexpr (kTiledLayout) {
+            if (c.k <= 8)
+                return launch_probe_tiled<FLAVOR, LAYOUT, 8>(k_, o_, key_len, n_, c, words, out_, st, g);
+            if constexpr (LAYOUT == kFixed32)
+                return launch_probe_tiled<FLAVOR, LAYOUT, 16>(k_, o_, key_len, n_, c, words, out_, st, g);
+        }
+        return fail(NB_ERR_UNSUPPORTED, "tiled probe: unsupported shape");
+    };
+    if (path == 2) return tiled(keys, offsets, n, out, none);
+    // auto: the sample, then both paths gated on its hit count
+    Workspace *ws;
+    int rc;
+    if ((rc = get_ws(st, &ws))) return rc;
+    {
+        std::lock_guard<std::mutex> lk(ws->mu);
+        if (!ws->probe_hits) NB_HIP(hipMalloc(&ws->probe_hits, 64));
+    }
+    const uint64_t S = kProbeSample;
+    NB_HIP(hipMemsetAsync(ws->probe_hits, 0, 4, st));
+    const ProbeGate sample{ws->probe_hits, nullptr, (uint32_t)S, 1};
+    const ProbeGate lane{nullptr, ws->probe_hits, (uint32_t)S, 1};
+    const ProbeGate tile{nullptr, ws->probe_hits, (uint32_t)S, 2};
+    const uint8_t *rk = offsets ? keys : keys + S * key_len;
+    const uint64_t *ro = offsets ? offsets + S : nullptr;
+    if ((rc = launch_probe_lane<FLAVOR, LAYOUT>(keys, offsets, key_len, S, c, words, out, st, sample)) ||
+        (rc = launch_probe_lane<FLAVOR, LAYOUT>(rk, ro, key_len, n - S, c, words, out + S, st, lane)))
+        return rc;
+    return tiled(rk, ro, n - S, out + S, tile);
+}
+
 template <int FLAVOR>
 int launch_probe_f(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                    const FilterConsts &c, const uint64_t *words, uint8_t *out, hipStream_t st) {
-    dim3 grid(grid_for(n)), block(kBlock);
-    const uint32_t *w32 = reinterpret_cast<const uint32_t *>(words);
     if (!offsets && key_len == 16 && (reinterpret_cast<uintptr_t>(keys) & 15) == 0)
-        hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, kFixed16>), grid, block, 0, st, keys,
-                           offsets, key_len, n, c, w32, out);
-    else if (!offsets && key_len == 32 && (reinterpret_cast<uintptr_t>(keys) & 15) == 0)
-        hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, kFixed32>), grid, block, 0, st, keys,
-                           offsets, key_len, n, c, w32, out);
-    else if (!offsets)
-        hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, kFixedStride>), grid, block, 0, st, keys,
-                           offsets, key_len, n, c, w32, out);
-    else
-        hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, kOffsets>), grid, block, 0, st, keys,
-                           offsets, key_len, n, c, w32, out);
-    NB_HIP(hipGetLastError());
-    return NB_OK;
+        return launch_probe_l<FLAVOR, kFixed16>(keys, offsets, key_len, n, c, words, out, st);
+    if (!offsets && key_len == 32 && (reinterpret_cast<uintptr_t>(keys) & 15) == 0)
+        return launch_probe_l<FLAVOR, kFixed32>(keys, offsets, key_len, n, c, words, out, st);
+    if (!offsets)
+        return launch_probe_l<FLAVOR, kFixedStride>(keys, offsets, key_len, n, c, words, out, st);
+    return launch_probe_l<FLAVOR, kOffsets>(keys, offsets, key_len, n, c, words, out, st);
 }
 
 std::atomic<uint64_t> g_device_builds{0};  // nb_device_build_count()
@@ -1928,6 +2229,7 @@ int nb_shutdown(void) {
             if (w->zeroed) (void)hipFree(w->zeroed);
             if (w->buckets) (void)hipFree(w->buckets);
             if (w->buckets2) (void)hipFree(w->buckets2);
+            if (w->probe_hits) (void)hipFree(w->probe_hits);
             delete w;
         }
         g_ws.clear();

@@ -1,0 +1,121 @@
+"""GPU parity of the batch probe (BloomFilter::possiblyContains, BloomFilter.cpp:67-80,
+callers SSTManager.cpp:203,224) on every path: the lane kernel (one lane per key,
+early exit), the tiled path (probe_bin_kernel + probe_tile_kernel: lookups binned by
+filter tile and tested in LDS) and auto (a sampled prefix picks the path on the
+device).  Bit-exact against oracle.probe on mixed present / absent batches; the
+tiled and lane answers equal each other at C4's full size."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import SEED, dev_probe, t_u8, t_u64  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev(built):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+def device_words(dev, buf, offs, key_len, n, m, k, flavor=0):
+    """The filter of the first n keys, built on the device (its parity is tested
+    elsewhere), as host words."""
+    import torch
+    import nasp_bloom as nbm
+    wt = torch.zeros(nbm.nwords(m), dtype=torch.int64, device=dev)
+    nbm.build_device(t_u8(buf, dev), t_u64(offs[:n + 1], dev) if offs is not None else None, key_len, n,
+                     m, k, SEED, flavor, wt)
+    torch.cuda.synchronize()
+    return wt.cpu().numpy().view(np.uint64)
+
+
+def shapes():
+    from nasp_bloom import synth
+    n = 4_500_000
+    f16 = synth.fixed_keys(n, 16, seed=5)
+    var, voffs = synth.var_keys(n, 8, 64)
+    f32 = synth.fixed_keys(n, 32, seed=6)
+    return {
+        "c4_fixed16": (f16, None, 16, n, 958_505_838, 7, 0),
+        "c3_varlen": (var, voffs, 0, n, 958_505_838, 7, 0),
+        "c2_fixed16_fnv": (f16, None, 16, n, 95_850_584, 7, 1),
+        "c5_fixed32_k10": (f32, None, 32, n, 2**32 - 1, 10, 0),
+    }
+
+
+@pytest.fixture(scope="module")
+def probe_shapes():
+    return shapes()
+
+
+@pytest.mark.parametrize("path", ["lane", "tiled", "auto"])
+@pytest.mark.parametrize("shape", ["c4_fixed16", "c3_varlen", "c2_fixed16_fnv", "c5_fixed32_k10"])
+@pytest.mark.parametrize("present_first", [True, False])
+def test_probe_paths_match_oracle(dev, oracle, knobs, probe_shapes, path, shape, present_first):
+    """A filter of 60 % of the batch's keys, probed over all of them: present keys,
+    absent keys and the filter's false positives, bit-exact on every path.  With the
+    present keys first, auto's sample sees hits (tiled); absent first, misses (lane)."""
+    buf, offs, kl, n, m, k, fl = probe_shapes[shape]
+    knobs(NB_PROBE_PATH=path)
+    npres = int(n * 0.6)
+    if present_first:
+        words = device_words(dev, buf, offs, kl, npres, m, k, fl)
+    else:  # the filter of the last 60 % of the keys
+        if offs is None:
+            words = device_words(dev, buf[(n - npres) * kl:], None, kl, npres, m, k, fl)
+        else:
+            sh = offs[n - npres:] - offs[n - npres]
+            words = device_words(dev, buf[int(offs[n - npres]):], sh, 0, npres, m, k, fl)
+    got = dev_probe(dev, buf, offs, kl, n, m, k, SEED, words, fl)
+    want = oracle.probe(fl, buf, offs, kl, n, m, k, SEED, words)
+    np.testing.assert_array_equal(got, want)
+    lo, hi = (0, npres) if present_first else (n - npres, n)
+    assert got[lo:hi].all()
+    assert got.mean() - 0.6 < 0.02  # the absent 40 %: false positives only
+
+
+def test_tiled_probe_overflow_and_small_filter(dev, oracle, knobs):
+    """Duplicated keys overflow the probe's buckets (those entries are tested in the
+    bin kernel instead); a small filter (few, small tiles); k = 1 and k = 8."""
+    from nasp_bloom import synth
+    knobs(NB_PROBE_PATH="tiled")
+    n = 400_000
+    dup = np.zeros(n * 16 + 16, np.uint8)
+    dup[: 16 * 1000] = synth.fixed_keys(1000, 16)[: 16 * 1000]
+    for m, k in ((958_505_838, 7), (1_000_003, 8), (2**20 + 5, 1)):
+        words = oracle.build(0, dup, None, 16, 2000, m, k, SEED)  # 1000 distinct + zero keys
+        got = dev_probe(dev, dup, None, 16, n, m, k, SEED, words)
+        np.testing.assert_array_equal(got, oracle.probe(0, dup, None, 16, n, m, k, SEED, words))
+        assert got.all()
+    vb, vo = synth.var_keys(300_000, 0, 70)  # empty keys included
+    words = oracle.build(1, vb, vo, 0, 150_000, 5_000_011, 7, SEED)
+    np.testing.assert_array_equal(dev_probe(dev, vb, vo, 0, 300_000, 5_000_011, 7, SEED, words, 1),
+                                  oracle.probe(1, vb, vo, 0, 300_000, 5_000_011, 7, SEED, words))
+
+
+def test_tiled_probe_c4_full_size(dev, knobs):
+    """C4's 100M-key filter probed with 100M present keys and 100M absent ones: the
+    tiled path answers 1 for every present key and exactly what the lane path
+    answers for the absent ones (the filter's false positives)."""
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    w = synth.C4
+    g = torch.Generator(device=dev).manual_seed(synth.SEED + 9)
+    kt = torch.randint(0, 256, (2 * w.n * 16,), dtype=torch.uint8, device=dev, generator=g)
+    words = torch.zeros(nbm.nwords(w.m), dtype=torch.int64, device=dev)
+    nbm.build_device(kt, None, 16, w.n, w.m, w.k, SEED, 0, words, overwrite=True)
+    outs = {}
+    for path in ("tiled", "lane"):
+        knobs(NB_PROBE_PATH=path)
+        out = torch.zeros(2 * w.n, dtype=torch.uint8, device=dev)
+        nbm.probe_device(kt, None, 16, 2 * w.n, w.m, w.k, SEED, 0, words, out)
+        torch.cuda.synchronize()
+        outs[path] = out
+    assert int(outs["tiled"][: w.n].min()) == 1
+    assert torch.equal(outs["tiled"], outs["lane"])
+    fp = float(outs["lane"][w.n:].float().mean())
+    assert 0.008 < fp < 0.012
