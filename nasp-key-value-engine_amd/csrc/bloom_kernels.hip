@@ -475,7 +475,7 @@ struct TileScratch {
 // cnt[t] and one add (plus the store).  The run table goes over S: byte offsets
 // into the buckets (write-out = one add and one 32-bit-offset store per word)
 // while the buckets stay under 4 GiB.
-template <int NT, int KPT, int KR, typename ENTRY>
+template <int NT, int KPT, int KR, typename ENTRY, int KX = 0>
 __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_off_words,
                                                    const TileCfg &tc, const TileScratch &sc,
                                                    ENTRY *__restrict__ buckets, uint64_t base,
@@ -546,7 +546,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
         if (base + (uint64_t)p * NT + tid < n) {
 #pragma unroll
             for (int j = 0; j < KR; ++j)
-                if (j < (int)k) {
+                if (KX ? j < KX : j < (int)k) {
                     const uint32_t h = pk[p][j];
                     lds_at(lds_at(h >> 16) + (h & 0xffffu)) = ridx[p][j];
                 }
@@ -725,7 +725,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
 // generator's start state (6 registers per key) is kept and the placement
 // regenerates the indices.  kid[p]: the key (index in the launch) slot p of this
 // lane hashed -- staged variable-length keys are hashed in a permuted order.
-template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR>
+template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR, int KX = 0>
 struct BinPhase1 {
     static constexpr int kR = KR > 0 ? KR : 1;
     IndexGen gen[KPT];
@@ -757,7 +757,7 @@ struct BinPhase1 {
             if (KR > 0) {
 #pragma unroll
                 for (int j = 0; j < kR; ++j) {
-                    if (j < (int)c.k) {
+                    if (KX ? j < KX : j < (int)c.k) {
                         if (j) g.next(c);
                         ridx[p][j] = g.r;
                         rank[p][j] = NB_DIAG_NOCOUNT ? g.r : atomicAdd(&cnt[g.r >> ts], 4u);
@@ -911,7 +911,7 @@ struct BinPhase1 {
 #define NB_BIN_MIN_WAVES(NT) (2 * (NT) / 256)
 #endif
 template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY, int NT = kBinThreads,
-          bool STAGE = !vec_layout(LAYOUT), int KR = 0>
+          bool STAGE = !vec_layout(LAYOUT), int KR = 0, int KX = 0>
 __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
     uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc, ENTRY *__restrict__ buckets) {
@@ -936,18 +936,18 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     // initialisation and its barrier
     const uint64_t base = (uint64_t)blockIdx.x * (KPT * NT);
     constexpr int kR = KR > 0 ? KR : 1;
-    BinPhase1<FLAVOR, LAYOUT, KPT, NT, STAGE, KR> ph;
+    BinPhase1<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, KX> ph;
     ph.run(keys, offsets, key_len, n, c, tc.ts, T, cnt, sorted, wave_sums + NT / 64 + 1, base);
     IndexGen (&gen)[KPT] = ph.gen;
     const uint32_t (&ridx)[KPT][kR] = ph.ridx;
     const uint32_t (&rank)[KPT][kR] = ph.rank;
     if (NB_DIAG_STOP(1)) return;
     if constexpr (pack_of<ENTRY>() > 1) {  // packed entries (host-checked T <= 2 NT, KR > 0)
-        bin_tail_two_tiles<NT, KPT, kR>(lds, bin_sort_offset_words(T), tc, sc, buckets, base, n,
+        bin_tail_two_tiles<NT, KPT, kR, ENTRY, KX>(lds, bin_sort_offset_words(T), tc, sc, buckets, base, n,
                                         c.k, ridx, rank);
     } else {
         if (NB_TWO_TILE && KR > 0 && T <= 2 * NT) {  // block-uniform: the common case (C2)
-            bin_tail_two_tiles<NT, KPT, kR>(lds, bin_sort_offset_words(T), tc, sc, buckets, base,
+            bin_tail_two_tiles<NT, KPT, kR, ENTRY, KX>(lds, bin_sort_offset_words(T), tc, sc, buckets, base,
                                             n, c.k, ridx, rank);
             return;
         }
@@ -993,7 +993,7 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
                 if (i < n) {
 #pragma unroll
                     for (int j = 0; j < kR; ++j)
-                        if (j < (int)c.k)
+                        if (KX ? j < KX : j < (int)c.k)
                             sorted[S[ridx[p][j] >> tc.ts] + ((rank[p][j] & 0xffffu) >> 2)] = ridx[p][j];
                 }
             }
@@ -1726,7 +1726,7 @@ int launch_atomic(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len
     return NB_OK;
 }
 
-template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY, int NT, bool STAGE, int KR>
+template <int FLAVOR, int LAYOUT, int KPT, typename ENTRY, int NT, bool STAGE, int KR, int KX>
 int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                    const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st,
                    uint64_t chunk, const TileCfg &tc) {
@@ -1743,7 +1743,7 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(NT));
     const size_t bin_lds = (size_t)bin_sort_offset_words(tc.T) * 4 + sort_bytes;
     const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
-    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, ENTRY, NT, STAGE, KR>;
+    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, ENTRY, NT, STAGE, KR, KX>;
     auto tile_ow = bloom_tile_or_kernel<ENTRY, true>;
     auto tile_or = bloom_tile_or_kernel<ENTRY, false>;
     if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(tile_ow, tile_lds)) ||
@@ -1779,7 +1779,7 @@ bool two_level_pack5() { return knob(nb::kKnobPack5) != 0; }
 // The two-level build (see bloom_rebin_kernel): per chunk, the bin kernel into
 // super tiles, the re-bin into fine tiles, the tile kernel on the fine tiles.
 // E1: pass-1 entry type (Pack5 or uint32_t); t1 comes with its capacity in entries.
-template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR, typename E1>
+template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR, int KX, typename E1>
 int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                      const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st,
                      uint64_t chunk, const TileCfg &t1e, const TileCfg &t2) {
@@ -1822,7 +1822,7 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
     const size_t bin_lds = (size_t)bin_sort_offset_words(t1.T) * 4 + sort_bytes;
     const size_t rebin_lds = ((size_t)rebin_span<IN5>() + 2 * kSuperFine) * 4;
     const size_t tile_lds = ((size_t)1 << (t2.ts - 3)) + (2 * kShards + 1) * 4;
-    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, E1, NT, STAGE, KR>;
+    auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, E1, NT, STAGE, KR, KX>;
     auto rebin = pack ? bloom_rebin_kernel<true, IN5> : bloom_rebin_kernel<false, IN5>;
     auto tile_ow = pack ? tile_kernel_of<uint64_t, true>() : tile_kernel_of<uint32_t, true>();
     auto tile_or = pack ? tile_kernel_of<uint64_t, false>() : tile_kernel_of<uint32_t, false>();
@@ -1852,7 +1852,7 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
     return NB_OK;
 }
 
-template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR>
+template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR, int KX = 0>
 int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                  const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st) {
     constexpr uint64_t kpb = (uint64_t)KPT * NT;
@@ -1869,16 +1869,16 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
         tc = choose_tiles(c.fm.m, chunk, c.k);
         if constexpr (KR > 0) {
             if (two_level_pack5())  // 2^(ts+5)-bit super tiles: 25-bit offsets
-                return launch_two_level<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, Pack5>(
+                return launch_two_level<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, KX, Pack5>(
                     keys, offsets, key_len, n, c, words, overwrite, st, chunk,
                     super_tiles(tc, c.fm.m, chunk, c.k, 5), tc);
         }
-        return launch_two_level<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, uint32_t>(
+        return launch_two_level<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, KX, uint32_t>(
             keys, offsets, key_len, n, c, words, overwrite, st, chunk,
             super_tiles(tc, c.fm.m, chunk, c.k, 6), tc);
     }
     if (tc.ts <= 16 && knob(nb::kKnobEntry32) == 0)
-        return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint16_t, NT, STAGE, KR>(
+        return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint16_t, NT, STAGE, KR, KX>(
             keys, offsets, key_len, n, c, words, overwrite, st, chunk, tc);
     if constexpr (KR > 0) {
         // 17-20-bit in-tile offsets: three per 64-bit bucket word (the two-tile
@@ -1898,11 +1898,11 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
             const uint64_t capw = ((uint64_t)tc.cap + 2 * bps + 2) / 3;
             TileCfg tp = tc;
             tp.cap = (uint32_t)std::min<uint64_t>((capw + 7) & ~7ull, 0xFFFFFFC0ull);
-            return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint64_t, NT, STAGE, KR>(
+            return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint64_t, NT, STAGE, KR, KX>(
                 keys, offsets, key_len, n, c, words, overwrite, st, chunk, tp);
         }
     }
-    return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint32_t, NT, STAGE, KR>(
+    return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint32_t, NT, STAGE, KR, KX>(
         keys, offsets, key_len, n, c, words, overwrite, st, chunk, tc);
 }
 
@@ -1917,6 +1917,21 @@ int launch_build_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         // and their in-tile ranks kept in registers while k <= 16 (NB_RANK=0: the
         // regenerate-and-recount variant, kept for A/B)
         const bool rank = knob(nb::kKnobRank) != 0;
+        // the parity flavours' common k (7 = the reference's k at p = 0.01; 10 = C5's)
+        // as a compile-time constant: index loops without per-index k checks, and
+        // exactly k rank registers per key (NB_KEXACT=0: the k <= 8 / 16 kernels)
+        constexpr bool kParity = FLAVOR != NB_FLAVOR_MURMUR3_X64_128;
+        const bool exact = kParity && rank && knob(nb::kKnobKExact) != 0;
+        if constexpr (kParity && (LAYOUT == kFixed16 || LAYOUT == kOffsets)) {
+            if (exact && c.k == 7)
+                return launch_tiled<FLAVOR, LAYOUT, kBinKPT, kBinThreads, !vec_layout(LAYOUT), 7, 7>(
+                    keys, offsets, key_len, n, c, words, overwrite, st);
+        }
+        if constexpr (kParity && LAYOUT == kFixed32) {
+            if (exact && c.k == 10)
+                return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, false, 10, 10>(
+                    keys, offsets, key_len, n, c, words, overwrite, st);
+        }
         if constexpr (vec_layout(LAYOUT)) {
             if (c.k <= 8)
                 return rank ? launch_tiled<FLAVOR, LAYOUT, kBinKPT, kBinThreads, false, 8>(

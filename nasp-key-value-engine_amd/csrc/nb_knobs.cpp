@@ -22,7 +22,8 @@ constexpr KnobDef kDefs[nb::kKnobCount] = {
     {"NB_BUILD_PATH", 0},    {"NB_PACK", 1},        {"NB_TILE_BITS", 0},
     {"NB_SHARDS", 8},        {"NB_CHUNK_KEYS", 0},  {"NB_TWO_LEVEL", 1},
     {"NB_PACK5", 1},         {"NB_ENTRY32", 0},     {"NB_RANK", 1},
-    {"NB_FIXED32", 1},       {"NB_FPMOD", 1},       {"NB_SHARDED_STAGE", 0},
+    {"NB_FIXED32", 1},       {"NB_FPMOD", 1},       {"NB_KEXACT", 1},
+    {"NB_SHARDED_STAGE", 0},
     {"NB_PROBE_PATH", 0},    {"NB_FAIL_BUILDS", 0}, {"NB_FAIL_MERKLES", 0},
 };
 

@@ -26,6 +26,7 @@ enum Knob : int {
     kKnobRank,          // NB_RANK           1: indices + ranks kept in registers (k <= 16)
     kKnobFixed32,       // NB_FIXED32        1: register path for 16-byte-aligned 32-byte keys
     kKnobFpMod,         // NB_FPMOD          1: f64-quotient remainders
+    kKnobKExact,        // NB_KEXACT         1: bin kernels specialised for k = 7 / 10
     kKnobShardedStage,  // NB_SHARDED_STAGE  1: nb_build_sharded stages every merge source
     kKnobProbePath,     // NB_PROBE_PATH     0 auto | 1 "lane" (one lane per key) | 2 "tiled"
     kKnobFailBuilds,    // NB_FAIL_BUILDS    fault injection: the next N device builds fail
