@@ -1377,6 +1377,7 @@ __global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
 // Present keys cost no stores at all; an absent key costs one store per zero bit
 // (~k/2), which is why absent-heavy batches keep the lane path (ProbeGate).
 constexpr int kProbeThreads = 1024;
+constexpr uint64_t kProbeBinGrid = 2048;  // probe_bin_kernel blocks at most (it loops)
 
 __host__ __device__ constexpr uint32_t probe_sort_offset_words(uint32_t T) {
     return (4 * T + 32 + 3) & ~3u;  // cnt | S | GX | L | wave_sums, 16-byte aligned
@@ -1395,45 +1396,52 @@ __global__ __launch_bounds__(kProbeThreads, 2) void probe_bin_kernel(
     uint32_t *wave_sums = lds + 4 * T;  // [NT/64 + 2]
     uint32_t *sidx = lds + probe_sort_offset_words(T);  // [NT * k] indices, sorted by tile
     uint32_t *skid = sidx + NT * k;                     // [NT * k] their keys
-    const uint64_t base = (uint64_t)blockIdx.x * NT;
-    BinPhase1<FLAVOR, LAYOUT, 1, NT, STAGE, KR> ph;
-    ph.run(keys, offsets, key_len, n, c, tc.ts, T, cnt, sidx, wave_sums + NT / 64 + 1, base);
-    const bool valid = base + tid < n;  // (staged keys: the valid ones fill the first slots)
-    if (valid) out[ph.kid[0]] = 1;
-    // counts from the placement handles (A_t << 16 | 4 rank, see BinPhase1)
-    for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << 16)) >> 2;
-    __syncthreads();
-    const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
-    // reserve a run in every touched tile's bucket shard; GX[t] = its first entry
-    // minus the run's local start, L[t] = the first local position past capacity
-    const uint32_t shard = blockIdx.x & (tc.G - 1);
-    uint32_t *cur = sc.gcur + (size_t)shard * T;
-    for (uint32_t t = tid; t < T; t += NT) {
-        const uint32_t h = cnt[t], g = h ? atomicAdd(&cur[t], h) : 0u;
-        GX[t] = (t * tc.G + shard) * tc.cap + g - S[t];
-        L[t] = S[t] + (g < tc.cap ? tc.cap - g : 0u);
-    }
-    // placement (the reservations' round trips overlap it)
-    if (valid) {
-#pragma unroll
-        for (int j = 0; j < KR; ++j)
-            if (j < (int)k) {
-                const uint32_t pos = S[ph.ridx[0][j] >> tc.ts] + ((ph.rank[0][j] & 0xffffu) >> 2);
-                sidx[pos] = ph.ridx[0][j];
-                skid[pos] = (uint32_t)ph.kid[0];
-            }
-    }
-    __syncthreads();
-    // write-out: one 64-bit entry per index, runs contiguous; an entry past its
-    // bucket's capacity (pathological duplicates only) is tested right here
-    const uint32_t msk = (1u << tc.ts) - 1;
-    for (uint32_t q = tid; q < total; q += NT) {
-        const uint32_t v = sidx[q], t = v >> tc.ts, kq = skid[q];
-        if (q < L[t]) {
-            buckets[(uint32_t)(GX[t] + q)] = ((uint64_t)kq << 32) | (v & msk);
-        } else if (!((words[v >> 6] >> (v & 63)) & 1u)) {
-            out[kq] = 0;
+    // a capped grid looping over the batch's NT-key blocks: a closed gate (auto
+    // mode chose the lane path) then costs a few thousand no-op blocks, not one per
+    // 1 024 keys
+    const uint64_t nvb = (n + NT - 1) / NT;
+    for (uint64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
+        const uint64_t base = vb * NT;
+        BinPhase1<FLAVOR, LAYOUT, 1, NT, STAGE, KR> ph;
+        ph.run(keys, offsets, key_len, n, c, tc.ts, T, cnt, sidx, wave_sums + NT / 64 + 1, base);
+        const bool valid = base + tid < n;  // (staged keys: the valid ones fill the first slots)
+        if (valid) out[ph.kid[0]] = 1;
+        // counts from the placement handles (A_t << 16 | 4 rank, see BinPhase1)
+        for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << 16)) >> 2;
+        __syncthreads();
+        const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
+        // reserve a run in every touched tile's bucket shard; GX[t] = its first entry
+        // minus the run's local start, L[t] = the first local position past capacity
+        const uint32_t shard = (uint32_t)vb & (tc.G - 1);
+        uint32_t *cur = sc.gcur + (size_t)shard * T;
+        for (uint32_t t = tid; t < T; t += NT) {
+            const uint32_t h = cnt[t], g = h ? atomicAdd(&cur[t], h) : 0u;
+            GX[t] = (t * tc.G + shard) * tc.cap + g - S[t];
+            L[t] = S[t] + (g < tc.cap ? tc.cap - g : 0u);
         }
+        // placement (the reservations' round trips overlap it)
+        if (valid) {
+#pragma unroll
+            for (int j = 0; j < KR; ++j)
+                if (j < (int)k) {
+                    const uint32_t pos = S[ph.ridx[0][j] >> tc.ts] + ((ph.rank[0][j] & 0xffffu) >> 2);
+                    sidx[pos] = ph.ridx[0][j];
+                    skid[pos] = (uint32_t)ph.kid[0];
+                }
+        }
+        __syncthreads();
+        // write-out: one 64-bit entry per index, runs contiguous; an entry past its
+        // bucket's capacity (pathological duplicates only) is tested right here
+        const uint32_t msk = (1u << tc.ts) - 1;
+        for (uint32_t q = tid; q < total; q += NT) {
+            const uint32_t v = sidx[q], t = v >> tc.ts, kq = skid[q];
+            if (q < L[t]) {
+                buckets[(uint32_t)(GX[t] + q)] = ((uint64_t)kq << 32) | (v & msk);
+            } else if (!((words[v >> 6] >> (v & 63)) & 1u)) {
+                out[kq] = 0;
+            }
+        }
+        __syncthreads();  // the next block's counters and sort area reuse the LDS
     }
 }
 
@@ -2033,8 +2041,9 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
         const uint64_t cn = std::min(chunk, n - done);
         const uint8_t *ck = offsets ? keys : keys + done * key_len;
         const uint64_t *co = offsets ? offsets + done : nullptr;
-        hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + NT - 1) / NT)), dim3(NT), bin_lds, st, ck, co,
-                           key_len, cn, c, tc, sc, bk, words, out + done, gate);
+        hipLaunchKernelGGL(bin, dim3((uint32_t)std::min<uint64_t>((cn + NT - 1) / NT, kProbeBinGrid)),
+                           dim3(NT), bin_lds, st, ck, co, key_len, cn, c, tc, sc, bk, words,
+                           out + done, gate);
         NB_HIP(hipGetLastError());
         hipLaunchKernelGGL(tile, dim3(tc.T), dim3(kTileThreads), tile_lds, st, tc, sc,
                            (const uint64_t *)bk, words, nwords, out + done, gate);

@@ -50,38 +50,53 @@ def _hip_merge(dst: torch.Tensor, recv: torch.Tensor, nsrc: int, stride: int) ->
 
 
 def merge_partials(partial: torch.Tensor, m: int, group=None, all_gather: bool = True,
-                   merge_fn: Callable | None = None, exchange_single: bool = False) -> torch.Tensor:
+                   merge_fn: Callable | None = None, exchange_single: bool = False,
+                   comm_device=None) -> torch.Tensor:
     """OR-merge every rank's full-size partial filter (int64 tensor of >= world*S
     words, padding zero).  Returns the whole merged filter (all_gather=True) or this
-    rank's owned slice of S words.  With one rank the partial already is the filter
-    and no collective runs (exchange_single=True forces the all-to-all / OR /
-    all-gather sequence anyway, for tests of the RCCL path on a one-GPU box)."""
+    rank's owned slice of S words (words [rank*S, (rank+1)*S) of the filter).  With
+    one rank the partial already is the filter and no collective runs
+    (exchange_single=True forces the all-to-all / OR / all-gather sequence anyway, for
+    tests of the RCCL path on a one-GPU box).  comm_device: where the exchanged
+    slices live for the collectives (default: the partial's device, i.e. RCCL over
+    xGMI); "cpu" routes them through host copies, so a gloo group -- e.g. ranks that
+    share one GPU -- runs the same sequence with the HIP build and OR kernels."""
     world = dist.get_world_size(group)
     S = slice_words(m, world)
     if partial.numel() < world * S:
         raise ValueError("partial filter must be padded to world * slice_words(m) words")
     if world == 1 and not exchange_single:
         return partial[:S]
+    cd = partial.device if comm_device is None else torch.device(comm_device)
     send = partial[: world * S].contiguous()
-    recv = torch.empty_like(send)
-    dist.all_to_all_single(recv, send, group=group)          # recv[j*S:(j+1)*S] = slice of rank j
+    send_c = send if cd == send.device else send.to(cd)
+    recv_c = torch.empty_like(send_c)
+    dist.all_to_all_single(recv_c, send_c, group=group)     # recv[j*S:(j+1)*S] = slice of rank j
+    recv = recv_c if cd == partial.device else recv_c.to(partial.device)
     owned = torch.zeros(S, dtype=partial.dtype, device=partial.device)
     (merge_fn or _hip_merge)(owned, recv, world, S)
     if not all_gather:
         return owned
-    full = torch.empty(world * S, dtype=partial.dtype, device=partial.device)
-    dist.all_gather_into_tensor(full, owned, group=group)
-    return full
+    owned_c = owned if cd == partial.device else owned.to(cd)
+    full_c = torch.empty(world * S, dtype=partial.dtype, device=cd)
+    dist.all_gather_into_tensor(full_c, owned_c, group=group)
+    return full_c if cd == partial.device else full_c.to(partial.device)
 
 
 def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len: int, n: int,
                       m: int, k: int, seed: int, flavor: int, group=None,
                       all_gather: bool = True, build_fn: Callable | None = None,
                       merge_fn: Callable | None = None, stream=None,
-                      exchange_single: bool = False) -> torch.Tensor:
+                      exchange_single: bool = False, comm_device=None,
+                      host_out: torch.Tensor | None = None) -> torch.Tensor:
     """Cooperative single-filter build.  `keys`/`offsets` hold THIS rank's key range
     (offsets relative to `keys`, n+1 entries; or fixed key_len).  Every rank passes
-    the same (m, k, seed, flavor)."""
+    the same (m, k, seed, flavor).  all_gather=False leaves each rank with its owned
+    slice only (words [rank*S, (rank+1)*S), S = slice_words(m, world)); with
+    `host_out` (a host tensor of >= S int64 words, pinned for an asynchronous copy)
+    that slice is downloaded into it -- the filter then ends in host memory, each
+    owner holding its part of SSTable::build's filter block (SURVEY §5: per-slice
+    D2H instead of an all-gather)."""
     world = dist.get_world_size(group)
     S = slice_words(m, world)
     if build_fn is None:
@@ -95,8 +110,15 @@ def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len:
                      overwrite=True)
     else:
         build_fn(keys, offsets, key_len, n, m, k, seed, flavor, partial)
-    return merge_partials(partial, m, group=group, all_gather=all_gather, merge_fn=merge_fn,
-                          exchange_single=exchange_single)
+    out = merge_partials(partial, m, group=group, all_gather=all_gather and host_out is None,
+                         merge_fn=merge_fn, exchange_single=exchange_single,
+                         comm_device=comm_device)
+    if host_out is not None:
+        if host_out.numel() < out.numel():
+            raise ValueError("host_out holds fewer words than the owned slice")
+        host_out[: out.numel()].copy_(out, non_blocking=host_out.is_pinned())
+        return host_out[: out.numel()]
+    return out
 
 
 def build_independent(keys: torch.Tensor, offsets: torch.Tensor | None, key_len: int, n: int,
