@@ -628,7 +628,7 @@ def test_c4_full_size_properties(dev, oracle):
 
 def test_c5_full_size_properties(dev, oracle):
     """C5 at its full size on one GPU: 1B x 32 B keys, k = 10, m = 2^32 - 1 (the
-    two-level path in five 200M-key passes).  (1) OR of 4 shard builds == whole
+    two-level path in eight 125M-key passes).  (1) OR of 4 shard builds == whole
     build, (2) every key probes positive, (3) fill matches 1 - exp(-kn/m), (4)
     bit-exact against the (threaded) oracle."""
     import torch
