@@ -249,15 +249,19 @@ __global__ __launch_bounds__(kBlock) void bloom_build_atomic_kernel(
 // choice needs no host synchronisation and the launch sequence stays
 // graph-capturable.
 struct ProbeGate {
-    uint32_t *hits;          // sample launch: add its positives here (nullptr: none)
-    const uint32_t *decide;  // nullptr: always run; else run iff the choice == want
+    uint32_t *hits;          // sample launch: its blocks' positive counts, one word per block
+    const uint32_t *decide;  // nullptr: always run; else the sample's counts: run iff the
+                             // choice they make == want
+    uint32_t blocks;         // sample blocks (words of decide)
     uint32_t sample;         // keys in the sample
     uint32_t want;           // 1 the lane path, 2 the tiled path
 };
 __device__ __forceinline__ bool gate_open(const ProbeGate &g) {
     if (!g.decide) return true;
+    uint32_t h = 0;  // uniform: scalar loads
+    for (uint32_t b = 0; b < g.blocks; ++b) h += g.decide[b];
     // tiled when at least half the sample was present
-    const uint32_t choice = 2ull * *g.decide >= g.sample ? 2u : 1u;
+    const uint32_t choice = 2ull * h >= g.sample ? 2u : 1u;
     return choice == g.want;
 }
 
@@ -283,9 +287,16 @@ __global__ __launch_bounds__(kBlock) void bloom_probe_kernel(
         out[i] = hit;
         hits += hit;
     }
-    if (gate.hits) {  // one atomic per wave
+    if (gate.hits) {  // the block's count (plain stores: nothing to zero beforehand)
+        __shared__ uint32_t wsum[kBlock / 64];
         for (int o = 32; o; o >>= 1) hits += __shfl_xor(hits, o);
-        if ((threadIdx.x & 63) == 0 && hits) atomicAdd(gate.hits, hits);
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = hits;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (int w = 0; w < kBlock / 64; ++w) t += wsum[w];
+            gate.hits[blockIdx.x] = t;
+        }
     }
 }
 
@@ -730,7 +741,7 @@ struct BinPhase1 {
     static constexpr int kR = KR > 0 ? KR : 1;
     IndexGen gen[KPT];
     uint32_t ridx[KPT][kR], rank[KPT][kR];
-    uint64_t kid[KPT];
+    uint32_t kid[KPT];  // (mod 2^32: the probe launches chunks of < 2^32 keys)
 
     __device__ __forceinline__ void run(const uint8_t *__restrict__ keys,
                                         const uint64_t *__restrict__ offsets, uint32_t key_len,
@@ -782,7 +793,7 @@ struct BinPhase1 {
             for (int p = 0; p < KPT; ++p)
                 if (base + (uint64_t)p * NT + tid < n) count_key(p, h1[p], h2[p]);
 #pragma unroll
-            for (int p = 0; p < KPT; ++p) kid[p] = base + (uint64_t)p * NT + tid;
+            for (int p = 0; p < KPT; ++p) kid[p] = (uint32_t)(base + (uint64_t)p * NT + tid);
         } else {
             // Variable-length (or odd fixed-length) keys, one sub-batch of NT keys at a
             // time: its keys are one contiguous byte range.  When that fits the stage
@@ -836,7 +847,7 @@ struct BinPhase1 {
                     for (uint32_t q = tid; q < nvec; q += NT) dst[q] = src[q];
                 }
                 uint32_t klo = (uint32_t)(b - kb0 + a0), klen = (uint32_t)(e - b);
-                kid[p] = i;
+                kid[p] = (uint32_t)i;
                 bool kvalid = i < n;
                 // counting sort of the sub-batch by word count (absent keys last): whole
                 // words for the libstdc++ dword path (its loop runs over whole words, then
@@ -866,7 +877,7 @@ struct BinPhase1 {
                     klo = info & 0xffffu;
                     klen = info >> 16;
                     kvalid = pb + src < n;  // == (i < n): the valid keys fill the first slots
-                    kid[p] = pb + src;
+                    kid[p] = (uint32_t)(pb + src);
                     if (tid < kLenClasses) lhist[tid] = 0u;  // read by all before the barrier above
                 }
                 if (kvalid) {
@@ -1377,14 +1388,13 @@ __global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
 // Present keys cost no stores at all; an absent key costs one store per zero bit
 // (~k/2), which is why absent-heavy batches keep the lane path (ProbeGate).
 constexpr int kProbeThreads = 1024;
-constexpr uint64_t kProbeBinGrid = 2048;  // probe_bin_kernel blocks at most (it loops)
 
 __host__ __device__ constexpr uint32_t probe_sort_offset_words(uint32_t T) {
     return (4 * T + 32 + 3) & ~3u;  // cnt | S | GX | L | wave_sums, 16-byte aligned
 }
 
 template <int FLAVOR, int LAYOUT, bool STAGE, int KR>
-__global__ __launch_bounds__(kProbeThreads, 2) void probe_bin_kernel(
+__global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) void probe_bin_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
     uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc, uint64_t *__restrict__ buckets,
     const uint64_t *__restrict__ words, uint8_t *__restrict__ out, ProbeGate gate) {
@@ -1396,52 +1406,45 @@ __global__ __launch_bounds__(kProbeThreads, 2) void probe_bin_kernel(
     uint32_t *wave_sums = lds + 4 * T;  // [NT/64 + 2]
     uint32_t *sidx = lds + probe_sort_offset_words(T);  // [NT * k] indices, sorted by tile
     uint32_t *skid = sidx + NT * k;                     // [NT * k] their keys
-    // a capped grid looping over the batch's NT-key blocks: a closed gate (auto
-    // mode chose the lane path) then costs a few thousand no-op blocks, not one per
-    // 1 024 keys
-    const uint64_t nvb = (n + NT - 1) / NT;
-    for (uint64_t vb = blockIdx.x; vb < nvb; vb += gridDim.x) {
-        const uint64_t base = vb * NT;
-        BinPhase1<FLAVOR, LAYOUT, 1, NT, STAGE, KR> ph;
-        ph.run(keys, offsets, key_len, n, c, tc.ts, T, cnt, sidx, wave_sums + NT / 64 + 1, base);
-        const bool valid = base + tid < n;  // (staged keys: the valid ones fill the first slots)
-        if (valid) out[ph.kid[0]] = 1;
-        // counts from the placement handles (A_t << 16 | 4 rank, see BinPhase1)
-        for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << 16)) >> 2;
-        __syncthreads();
-        const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
-        // reserve a run in every touched tile's bucket shard; GX[t] = its first entry
-        // minus the run's local start, L[t] = the first local position past capacity
-        const uint32_t shard = (uint32_t)vb & (tc.G - 1);
-        uint32_t *cur = sc.gcur + (size_t)shard * T;
-        for (uint32_t t = tid; t < T; t += NT) {
-            const uint32_t h = cnt[t], g = h ? atomicAdd(&cur[t], h) : 0u;
-            GX[t] = (t * tc.G + shard) * tc.cap + g - S[t];
-            L[t] = S[t] + (g < tc.cap ? tc.cap - g : 0u);
-        }
-        // placement (the reservations' round trips overlap it)
-        if (valid) {
+    const uint64_t base = (uint64_t)blockIdx.x * NT;
+    BinPhase1<FLAVOR, LAYOUT, 1, NT, STAGE, KR> ph;
+    ph.run(keys, offsets, key_len, n, c, tc.ts, T, cnt, sidx, wave_sums + NT / 64 + 1, base);
+    const bool valid = base + tid < n;  // (staged keys: the valid ones fill the first slots)
+    if (valid) out[ph.kid[0]] = 1;
+    // counts from the placement handles (A_t << 16 | 4 rank, see BinPhase1)
+    for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << 16)) >> 2;
+    __syncthreads();
+    const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
+    // reserve a run in every touched tile's bucket shard; GX[t] = its first entry
+    // minus the run's local start, L[t] = the first local position past capacity
+    const uint32_t shard = blockIdx.x & (tc.G - 1);
+    uint32_t *cur = sc.gcur + (size_t)shard * T;
+    for (uint32_t t = tid; t < T; t += NT) {
+        const uint32_t h = cnt[t], g = h ? atomicAdd(&cur[t], h) : 0u;
+        GX[t] = (t * tc.G + shard) * tc.cap + g - S[t];
+        L[t] = S[t] + (g < tc.cap ? tc.cap - g : 0u);
+    }
+    // placement (the reservations' round trips overlap it)
+    if (valid) {
 #pragma unroll
-            for (int j = 0; j < KR; ++j)
-                if (j < (int)k) {
-                    const uint32_t pos = S[ph.ridx[0][j] >> tc.ts] + ((ph.rank[0][j] & 0xffffu) >> 2);
-                    sidx[pos] = ph.ridx[0][j];
-                    skid[pos] = (uint32_t)ph.kid[0];
-                }
-        }
-        __syncthreads();
-        // write-out: one 64-bit entry per index, runs contiguous; an entry past its
-        // bucket's capacity (pathological duplicates only) is tested right here
-        const uint32_t msk = (1u << tc.ts) - 1;
-        for (uint32_t q = tid; q < total; q += NT) {
-            const uint32_t v = sidx[q], t = v >> tc.ts, kq = skid[q];
-            if (q < L[t]) {
-                buckets[(uint32_t)(GX[t] + q)] = ((uint64_t)kq << 32) | (v & msk);
-            } else if (!((words[v >> 6] >> (v & 63)) & 1u)) {
-                out[kq] = 0;
+        for (int j = 0; j < KR; ++j)
+            if (j < (int)k) {
+                const uint32_t pos = S[ph.ridx[0][j] >> tc.ts] + ((ph.rank[0][j] & 0xffffu) >> 2);
+                sidx[pos] = ph.ridx[0][j];
+                skid[pos] = ph.kid[0];
             }
+    }
+    __syncthreads();
+    // write-out: one 64-bit entry per index, runs contiguous; an entry past its
+    // bucket's capacity (pathological duplicates only) is tested right here
+    const uint32_t msk = (1u << tc.ts) - 1;
+    for (uint32_t q = tid; q < total; q += NT) {
+        const uint32_t v = sidx[q], t = v >> tc.ts, kq = skid[q];
+        if (q < L[t]) {
+            buckets[(uint32_t)(GX[t] + q)] = ((uint64_t)kq << 32) | (v & msk);
+        } else if (!((words[v >> 6] >> (v & 63)) & 1u)) {
+            out[kq] = 0;
         }
-        __syncthreads();  // the next block's counters and sort area reuse the LDS
     }
 }
 
@@ -1997,7 +2000,8 @@ TileCfg probe_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
 
 // Auto mode's sample (the first kProbeSample keys, probed by the lane kernel) and
 // the smallest batch the tiled path is considered for.
-constexpr uint64_t kProbeSample = 1 << 16;
+constexpr uint32_t kProbeSampleBlocks = 16;                 // one key per lane
+constexpr uint64_t kProbeSample = kProbeSampleBlocks * kBlock;  // 4 096 keys
 constexpr uint64_t kProbeTiledMin = 1 << 22;
 
 template <int FLAVOR, int LAYOUT>
@@ -2041,9 +2045,8 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
         const uint64_t cn = std::min(chunk, n - done);
         const uint8_t *ck = offsets ? keys : keys + done * key_len;
         const uint64_t *co = offsets ? offsets + done : nullptr;
-        hipLaunchKernelGGL(bin, dim3((uint32_t)std::min<uint64_t>((cn + NT - 1) / NT, kProbeBinGrid)),
-                           dim3(NT), bin_lds, st, ck, co, key_len, cn, c, tc, sc, bk, words,
-                           out + done, gate);
+        hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + NT - 1) / NT)), dim3(NT), bin_lds, st, ck, co,
+                           key_len, cn, c, tc, sc, bk, words, out + done, gate);
         NB_HIP(hipGetLastError());
         hipLaunchKernelGGL(tile, dim3(tc.T), dim3(kTileThreads), tile_lds, st, tc, sc,
                            (const uint64_t *)bk, words, nwords, out + done, gate);
@@ -2064,7 +2067,7 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     const uint32_t kmax = LAYOUT == kFixed32 ? 16u : 8u;
     const bool tiled_ok = kTiledLayout && c.k <= kmax &&
                           probe_tiles(c.fm.m, n, c.k).T <= kMaxTiles;
-    const ProbeGate none{nullptr, nullptr, 0, 0};
+    const ProbeGate none{nullptr, nullptr, 0, 0, 0};
     if (path == 1 || !tiled_ok || (path == 0 && n < kProbeTiledMin))
         return launch_probe_lane<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, out, st, none);
     auto tiled = [&](const uint8_t *k_, const uint64_t *o_, uint64_t n_, uint8_t *out_,
@@ -2078,23 +2081,26 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         return fail(NB_ERR_UNSUPPORTED, "tiled probe: unsupported shape");
     };
     if (path == 2) return tiled(keys, offsets, n, out, none);
-    // auto: the sample, then both paths gated on its hit count
+    // auto: the sample (one key per lane, one count per block), then both paths
+    // gated on its counts
     Workspace *ws;
     int rc;
     if ((rc = get_ws(st, &ws))) return rc;
     {
         std::lock_guard<std::mutex> lk(ws->mu);
-        if (!ws->probe_hits) NB_HIP(hipMalloc(&ws->probe_hits, 64));
+        if (!ws->probe_hits) NB_HIP(hipMalloc(&ws->probe_hits, kProbeSampleBlocks * 4));
     }
     const uint64_t S = kProbeSample;
-    NB_HIP(hipMemsetAsync(ws->probe_hits, 0, 4, st));
-    const ProbeGate sample{ws->probe_hits, nullptr, (uint32_t)S, 1};
-    const ProbeGate lane{nullptr, ws->probe_hits, (uint32_t)S, 1};
-    const ProbeGate tile{nullptr, ws->probe_hits, (uint32_t)S, 2};
+    const ProbeGate sample{ws->probe_hits, nullptr, kProbeSampleBlocks, (uint32_t)S, 1};
+    const ProbeGate lane{nullptr, ws->probe_hits, kProbeSampleBlocks, (uint32_t)S, 1};
+    const ProbeGate tile{nullptr, ws->probe_hits, kProbeSampleBlocks, (uint32_t)S, 2};
     const uint8_t *rk = offsets ? keys : keys + S * key_len;
     const uint64_t *ro = offsets ? offsets + S : nullptr;
-    if ((rc = launch_probe_lane<FLAVOR, LAYOUT>(keys, offsets, key_len, S, c, words, out, st, sample)) ||
-        (rc = launch_probe_lane<FLAVOR, LAYOUT>(rk, ro, key_len, n - S, c, words, out + S, st, lane)))
+    hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, LAYOUT>), dim3(kProbeSampleBlocks), dim3(kBlock), 0,
+                       st, keys, offsets, key_len, S, c, reinterpret_cast<const uint32_t *>(words),
+                       out, sample);
+    NB_HIP(hipGetLastError());
+    if ((rc = launch_probe_lane<FLAVOR, LAYOUT>(rk, ro, key_len, n - S, c, words, out + S, st, lane)))
         return rc;
     return tiled(rk, ro, n - S, out + S, tile);
 }
