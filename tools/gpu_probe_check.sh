@@ -1,0 +1,12 @@
+#!/bin/bash
+# Probe-path check (run under gpurun): the probe GPU tests, then every probe path's
+# rate on C4 and C3 (bench.py `probe` field).
+set -u
+mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread -k "probe" > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -le 1 ] || exit 1
+for w in c4 c3; do
+  timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline --no-host-path --no-c2 --steps 10 > gpurun_out/bench_probe_$w.json 2> gpurun_out/bench_probe_$w.err || exit 2
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[1], d['value'], d['roofline']['kernel_ms']); [print(' ', p, d['probe'][p]['present']['ms'], d['probe'][p]['absent']['ms']) for p in ('auto','lane','tiled')]" gpurun_out/bench_probe_$w.json
+done
+exit $rc
