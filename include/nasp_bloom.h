@@ -197,6 +197,15 @@ int nb_build_device_ex(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_
                        uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
                        uint64_t *d_words, uint32_t flags, void *stream);
 
+/* Batch probe, device-resident.  Large batches (>= 4M keys) of 16-, 32-byte or
+ * variable-length keys with k <= 8 (k <= 16 for 32-byte keys) may take the tiled
+ * path (lookups binned by filter tile and tested in LDS: ~4x the one-lane-per-key
+ * rate for present keys, ~half of it for absent ones); NB_PROBE_PATH=0 (auto)
+ * probes the first 4 096 keys one lane per key and picks the tiled path when at
+ * least half of them were present.  Auto synchronises `stream` once to read that
+ * sample (64 bytes) -- except while the stream is being captured into a graph,
+ * where both paths are launched and gated on the sample on the device.  Same
+ * answers on every path. */
 int nb_probe_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
                     uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
                     const uint64_t *d_words, uint8_t *d_out, void *stream);
