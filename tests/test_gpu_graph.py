@@ -61,3 +61,38 @@ def test_build_replayed_from_graph(dev, oracle, var):
         buf, offs = sets[i]
         want = oracle.build(0, buf, offs, kl, n, m, k, SEED)
         np.testing.assert_array_equal(words.cpu().numpy().view(np.uint64), want)
+
+
+@pytest.mark.parametrize("present", [True, False])
+def test_auto_probe_replayed_from_graph(dev, oracle, present):
+    """The auto probe under stream capture: no host read-back of its sample is
+    possible, so both paths are captured and gated on the sample on the device;
+    replays on present keys (tiled chosen) and on absent keys (lane chosen) give the
+    oracle's answers."""
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    n, m, k = 4_200_000, 40_250_003, 7
+    base = synth.fixed_keys(n, 16, seed=71)
+    words_np = oracle.build(0, base, None, 16, n, m, k, SEED)
+    other = synth.fixed_keys(n, 16, seed=72)
+    kt = torch.from_numpy(base).to(dev)
+    words = torch.from_numpy(words_np.view(np.int64)).to(dev)
+    out = torch.zeros(n, dtype=torch.uint8, device=dev)
+    st = torch.cuda.Stream(device=dev)
+    with nbm.knobs(NB_PROBE_PATH="auto"):
+        with torch.cuda.stream(st):  # warm-up: sizes the workspace for both paths
+            nbm.probe_device(kt, None, 16, n, m, k, SEED, 0, words, out, stream=st)
+        st.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=st):
+            nbm.probe_device(kt, None, 16, n, m, k, SEED, 0, words, out, stream=st)
+        keys = base if present else other
+        kt.copy_(torch.from_numpy(keys))
+        out.zero_()
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    np.testing.assert_array_equal(got, oracle.probe(0, keys, None, 16, n, m, k, SEED, words_np))
+    assert got.all() == present
