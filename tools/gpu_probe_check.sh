@@ -3,7 +3,7 @@
 # rate on C4 and C3 (bench.py `probe` field).
 set -u
 mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread -k "probe" > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 170 --timeout-method thread -k "probe or graph" > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -2 gpurun_out/pytest_gpu.log; [ $rc -le 1 ] || exit 1
 for w in c4 c3; do
   timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline --no-host-path --no-c2 --steps 10 > gpurun_out/bench_probe_$w.json 2> gpurun_out/bench_probe_$w.err || exit 2
