@@ -80,7 +80,7 @@ uint64_t nb_device_merkle_count(void);
  * it for the whole process afterwards (thread-safe).  Names: NB_BUILD_PATH
  * (0 auto, 1 atomic, 2 tiled), NB_PROBE_PATH (0 auto, 1 one lane per key, 2 tiled),
  * NB_PACK, NB_TILE_BITS, NB_SHARDS, NB_CHUNK_KEYS, NB_TWO_LEVEL, NB_PACK5,
- * NB_ENTRY32, NB_RANK, NB_FIXED32, NB_FPMOD, NB_KEXACT, NB_SHARDED_STAGE, NB_FAIL_BUILDS /
+ * NB_ENTRY32, NB_RANK, NB_FIXED32, NB_FPMOD, NB_KEXACT, NB_BIN_WIDE, NB_SHARDED_STAGE, NB_FAIL_BUILDS /
  * NB_FAIL_MERKLES (the next N device builds / trees fail with NB_ERR_HIP).
  * Unknown names: NB_ERR_ARG. */
 int nb_set_knob(const char *name, uint64_t value);

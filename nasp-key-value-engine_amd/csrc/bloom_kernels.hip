@@ -338,6 +338,7 @@ __host__ __device__ constexpr uint32_t pack_of() {
 }
 
 constexpr int kBinThreads = 1024;
+constexpr int kBinThreadsWide = 896;  // 32-byte keys at k = 10: 2 x 896 keys per block
 constexpr int kBinKPT = 2;       // keys per thread when k <= 8 (1 for larger k)
 constexpr int kTileThreads = 1024;
 constexpr int kTileUnroll = 4;   // 16-byte bucket loads in flight per lane
@@ -1940,6 +1941,12 @@ int launch_build_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
                     keys, offsets, key_len, n, c, words, overwrite, st);
         }
         if constexpr (kParity && LAYOUT == kFixed32) {
+            // (NB_BIN_WIDE: 896 threads x 2 keys, 1 792 keys per block -- two blocks of
+            // 10 indices per key still fit a CU's LDS -- amortising the per-block scan,
+            // reservations and pads over 1.75x the keys)
+            if (exact && c.k == 10 && knob(nb::kKnobBinWide) != 0)
+                return launch_tiled<FLAVOR, LAYOUT, 2, kBinThreadsWide, false, 10, 10>(
+                    keys, offsets, key_len, n, c, words, overwrite, st);
             if (exact && c.k == 10)
                 return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, false, 10, 10>(
                     keys, offsets, key_len, n, c, words, overwrite, st);

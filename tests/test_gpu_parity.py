@@ -751,19 +751,21 @@ def test_cooperative_build_single_rank(dev, oracle):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kexact", [0, 1])
-def test_exact_k_kernels(dev, oracle, knobs, kexact):
+@pytest.mark.parametrize("kexact,wide", [(0, 0), (1, 0), (1, 1)])
+def test_exact_k_kernels(dev, oracle, knobs, kexact, wide):
     """The bin kernels specialised for k = 7 (16-byte and variable-length keys) and
-    k = 10 (32-byte keys), and the general k <= 8 / k <= 16 kernels they replace
-    (NB_KEXACT=0), give the same bits as the oracle -- both flavours, chunked."""
+    k = 10 (32-byte keys; NB_BIN_WIDE=1: 1 792-key blocks), and the general
+    k <= 8 / k <= 16 kernels they replace (NB_KEXACT=0), give the same bits as the
+    oracle -- both flavours, chunked, single- and two-level."""
     from nasp_bloom import synth
-    knobs(NB_KEXACT=kexact, NB_BUILD_PATH="tiled", NB_CHUNK_KEYS=400_000)
+    knobs(NB_KEXACT=kexact, NB_BIN_WIDE=wide, NB_BUILD_PATH="tiled", NB_CHUNK_KEYS=400_000)
     n = 1_000_003
     f16 = synth.fixed_keys(n, 16, seed=21)
     vb, vo = synth.var_keys(n)
     f32 = synth.fixed_keys(n, 32, seed=22)
     for flavor in (0, 1):
         for buf, offs, kl, m, k in ((f16, None, 16, 958_505_838, 7), (vb, vo, 0, 95_850_584, 7),
-                                    (f32, None, 32, 2**32 - 1, 10), (f16, None, 16, 9_585_059, 7)):
+                                    (f32, None, 32, 2**32 - 1, 10), (f16, None, 16, 9_585_059, 7),
+                                    (f32, None, 32, 95_850_584, 10), (f32, None, 32, 2**31 - 1, 10)):
             got = dev_build(dev, buf, offs, kl, n, m, k, SEED, flavor=flavor)
             np.testing.assert_array_equal(got, oracle.build(flavor, buf, offs, kl, n, m, k, SEED))
