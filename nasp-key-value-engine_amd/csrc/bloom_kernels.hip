@@ -337,8 +337,11 @@ __host__ __device__ constexpr uint32_t pack_of() {
     return sizeof(ENTRY) == 16 ? 5u : sizeof(ENTRY) == 8 ? 3u : 1u;
 }
 
+// placement handles (BinPhase1): A_t << kHandleShift | 4 rank
+constexpr uint32_t kHandleShift = 18, kHandleMask = (1u << kHandleShift) - 1;
 constexpr int kBinThreads = 1024;
-constexpr int kBinThreadsWide = 896;  // 32-byte keys at k = 10: 2 x 896 keys per block
+constexpr int kBinThreadsWide = 896;    // 32-byte keys at k = 10: 2 x 896 keys per block
+constexpr int kBinThreads16Wide = 768;  // 16-byte keys at k = 7: 3 x 768 keys per block
 constexpr int kBinKPT = 2;       // keys per thread when k <= 8 (1 for larger k)
 constexpr int kTileThreads = 1024;
 constexpr int kTileUnroll = 4;   // 16-byte bucket loads in flight per lane
@@ -481,7 +484,7 @@ struct TileScratch {
 // two tiles 2 tid, 2 tid + 1 from the scan to the run table, so the scan is one
 // wave-scan round (no per-thread loops) and the reservations use the counts it
 // already holds; waves that own no tile skip the scan arithmetic.  The count
-// atomics of phase 1 returned placement handles pk = (4 t) << 16 | 4 rank (see
+// atomics of phase 1 returned placement handles pk = (4 t) << 18 | 4 rank (see
 // the kernel), so the run starts go over the counters themselves -- as byte
 // offsets of the sort area from `lds` -- and placement is one LDS read of
 // cnt[t] and one add (plus the store).  The run table goes over S: byte offsets
@@ -507,7 +510,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     constexpr uint32_t PK = pack_of<ENTRY>();
     constexpr bool PACK = PK > 1;
     auto slots = [](uint32_t c) { return PACK ? (c + PK - 1) / PK * PK : c; };
-    auto count_of = [&](uint32_t t) { return (cnt[t] - ((lds0 + 4 * t) << 16)) >> 2; };
+    auto count_of = [&](uint32_t t) { return (cnt[t] - ((lds0 + 4 * t) << kHandleShift)) >> 2; };
     // ---- phase 2: scan (one round), reservations
     const uint32_t t0 = 2 * tid;
     const bool scan_wave = wid * 128 < T;  // wave-uniform: the wave owns a tile
@@ -560,7 +563,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
             for (int j = 0; j < KR; ++j)
                 if (KX ? j < KX : j < (int)k) {
                     const uint32_t h = pk[p][j];
-                    lds_at(lds_at(h >> 16) + (h & 0xffffu)) = ridx[p][j];
+                    lds_at(lds_at(h >> kHandleShift) + (h & kHandleMask)) = ridx[p][j];
                 }
         }
     }
@@ -740,6 +743,8 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
 template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR, int KX = 0>
 struct BinPhase1 {
     static constexpr int kR = KR > 0 ? KR : 1;
+    static_assert(KR == 0 || (uint64_t)KPT * NT * KR < (1u << (kHandleShift - 2)),
+                  "a block's ranks must fit the placement handle's low bits");
     IndexGen gen[KPT];
     uint32_t ridx[KPT][kR], rank[KPT][kR];
     uint32_t kid[KPT];  // (mod 2^32: the probe launches chunks of < 2^32 keys)
@@ -752,7 +757,7 @@ struct BinPhase1 {
         const uint32_t tid = threadIdx.x;
         KeyBatch<FLAVOR, LAYOUT, KPT> kb;
         if (!STAGE) kb.load(keys, offsets, base + tid, NT, n);
-        for (uint32_t t = tid; t < T; t += NT) cnt[t] = KR > 0 ? lds_addr(cnt + t) << 16 : 0u;
+        for (uint32_t t = tid; t < T; t += NT) cnt[t] = KR > 0 ? lds_addr(cnt + t) << kHandleShift : 0u;
         if (tid == 0) *any_flag = 0u;  // block_any's flag
         if (STAGE && tid < kLenClasses)  // the staged keys' length-class counters (see below)
             sorted[(kStageBytes / 4) + 2 * NT + tid] = 0u;
@@ -937,13 +942,13 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     uint32_t *sorted = lds + bin_sort_offset_words(T);  // [KPB * k], 16-byte aligned
     const uint32_t tid = threadIdx.x;
     NB_DIAG_PROLOGUE();
-    // rank mode (KR > 0): cnt[t] starts at A_t << 16, A_t = the LDS byte address of
-    // cnt[t], and each index adds 4, so the count atomic returns its index's
-    // placement handle pk = A_t << 16 | 4 rank: where the run start will be (the
-    // scan writes it over cnt[t], as an absolute address) and the index's byte
-    // offset within the run.  4 rank <= 4 (2^14 - 1) stays in the low half; a full
-    // count of 2^14 carries into the high half, which the decode
-    // (cnt[t] - (A_t << 16)) >> 2 undoes.
+    // rank mode (KR > 0): cnt[t] starts at A_t << 18, A_t = the LDS byte address of
+    // cnt[t] (< 2^14: the counters lead the LDS, T <= 4 096), and each index adds 4,
+    // so the count atomic returns its index's placement handle pk = A_t << 18 |
+    // 4 rank: where the run start will be (the scan writes it over cnt[t], as an
+    // absolute address) and the index's byte offset within the run.  A block has
+    // fewer than 2^16 indices (static_assert in BinPhase1), so 4 rank stays in the
+    // low 18 bits and the decode (cnt[t] - (A_t << 18)) >> 2 is exact.
     // register-loaded keys: their loads are issued first, in flight across the LDS
     // initialisation and its barrier
     const uint64_t base = (uint64_t)blockIdx.x * (KPT * NT);
@@ -970,7 +975,7 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
         // the block's run minus S[t] (u32 wrap-around arithmetic), S[t] := first local
         // position past the bucket's capacity.
         if (KR > 0) {  // packed counters (see phase 1) back to counts
-            for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << 16)) >> 2;
+            for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << kHandleShift)) >> 2;
             __syncthreads();
         }
         const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
@@ -1006,7 +1011,7 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
 #pragma unroll
                     for (int j = 0; j < kR; ++j)
                         if (KX ? j < KX : j < (int)c.k)
-                            sorted[S[ridx[p][j] >> tc.ts] + ((rank[p][j] & 0xffffu) >> 2)] = ridx[p][j];
+                            sorted[S[ridx[p][j] >> tc.ts] + ((rank[p][j] & kHandleMask) >> 2)] = ridx[p][j];
                 }
             }
 #pragma unroll
@@ -1412,8 +1417,8 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
     ph.run(keys, offsets, key_len, n, c, tc.ts, T, cnt, sidx, wave_sums + NT / 64 + 1, base);
     const bool valid = base + tid < n;  // (staged keys: the valid ones fill the first slots)
     if (valid) out[ph.kid[0]] = 1;
-    // counts from the placement handles (A_t << 16 | 4 rank, see BinPhase1)
-    for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << 16)) >> 2;
+    // counts from the placement handles (A_t << kHandleShift | 4 rank, see BinPhase1)
+    for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << kHandleShift)) >> 2;
     __syncthreads();
     const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
     // reserve a run in every touched tile's bucket shard; GX[t] = its first entry
@@ -1430,7 +1435,7 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
 #pragma unroll
         for (int j = 0; j < KR; ++j)
             if (j < (int)k) {
-                const uint32_t pos = S[ph.ridx[0][j] >> tc.ts] + ((ph.rank[0][j] & 0xffffu) >> 2);
+                const uint32_t pos = S[ph.ridx[0][j] >> tc.ts] + ((ph.rank[0][j] & kHandleMask) >> 2);
                 sidx[pos] = ph.ridx[0][j];
                 skid[pos] = ph.kid[0];
             }
@@ -1935,6 +1940,13 @@ int launch_build_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         // exactly k rank registers per key (NB_KEXACT=0: the k <= 8 / 16 kernels)
         constexpr bool kParity = FLAVOR != NB_FLAVOR_MURMUR3_X64_128;
         const bool exact = kParity && rank && knob(nb::kKnobKExact) != 0;
+        if constexpr (kParity && LAYOUT == kFixed16) {
+            // (NB_BIN_WIDE: 768 threads x 3 keys, 2 304 keys per block -- two blocks
+            // still fit a CU's LDS at C4's 915 tiles -- at 6 waves per SIMD)
+            if (exact && c.k == 7 && knob(nb::kKnobBinWide) != 0)
+                return launch_tiled<FLAVOR, LAYOUT, 3, kBinThreads16Wide, false, 7, 7>(
+                    keys, offsets, key_len, n, c, words, overwrite, st);
+        }
         if constexpr (kParity && (LAYOUT == kFixed16 || LAYOUT == kOffsets)) {
             if (exact && c.k == 7)
                 return launch_tiled<FLAVOR, LAYOUT, kBinKPT, kBinThreads, !vec_layout(LAYOUT), 7, 7>(

@@ -27,7 +27,8 @@ enum Knob : int {
     kKnobFixed32,       // NB_FIXED32        1: register path for 16-byte-aligned 32-byte keys
     kKnobFpMod,         // NB_FPMOD          1: f64-quotient remainders
     kKnobKExact,        // NB_KEXACT         1: bin kernels specialised for k = 7 / 10
-    kKnobBinWide,       // NB_BIN_WIDE       1: 1 792-key bin blocks for 32-byte keys, k = 10
+    kKnobBinWide,       // NB_BIN_WIDE       1: larger bin blocks (2 304 keys for 16-byte keys
+                        //                   at k = 7, 1 792 for 32-byte keys at k = 10)
     kKnobShardedStage,  // NB_SHARDED_STAGE  1: nb_build_sharded stages every merge source
     kKnobProbePath,     // NB_PROBE_PATH     0 auto | 1 "lane" (one lane per key) | 2 "tiled"
     kKnobFailBuilds,    // NB_FAIL_BUILDS    fault injection: the next N device builds fail

@@ -769,3 +769,11 @@ def test_exact_k_kernels(dev, oracle, knobs, kexact, wide):
                                     (f32, None, 32, 95_850_584, 10), (f32, None, 32, 2**31 - 1, 10)):
             got = dev_build(dev, buf, offs, kl, n, m, k, SEED, flavor=flavor)
             np.testing.assert_array_equal(got, oracle.build(flavor, buf, offs, kl, n, m, k, SEED))
+    # duplicated keys: one block's indices pile into a few tiles (ranks up to
+    # KPT * NT * k - 1, the placement handles' widest case)
+    dup16 = np.zeros(300_000 * 16 + 16, np.uint8)
+    dup32 = np.zeros(300_000 * 32 + 16, np.uint8)
+    for buf, kl, m, k in ((dup16, 16, 1_000_003, 7), (dup32, 32, 1_000_003, 10),
+                          (dup32, 32, 2**32 - 1, 10)):
+        got = dev_build(dev, buf, None, kl, 300_000, m, k, SEED)
+        np.testing.assert_array_equal(got, oracle.build(0, buf, None, kl, 300_000, m, k, SEED))
