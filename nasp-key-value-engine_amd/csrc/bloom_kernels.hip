@@ -1588,6 +1588,15 @@ struct Workspace {
     size_t bucket2_bytes = 0;
     uint32_t *probe_hits = nullptr;       // the auto probe's sample counts (ProbeGate)
     uint32_t *probe_hits_host = nullptr;  // pinned copy of them
+    // pipelined two-level passes (NB_OVERLAP): a second stream for the re-bin + tile
+    // kernels, the odd passes' pass-1 buckets, super-tile cursors and spill scratch
+    hipStream_t aux = nullptr;
+    int aux_prio = 0;
+    hipEvent_t ev_bin[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr}, ev_start = nullptr;
+    uint32_t *zeroed_alt = nullptr;
+    size_t zeroed_alt_bytes = 0;
+    void *buckets_alt = nullptr;
+    size_t bucket_alt_bytes = 0;
 };
 std::mutex g_ws_mu;
 std::vector<Workspace *> g_ws;
@@ -1654,6 +1663,38 @@ int ws_reserve(Workspace &w, uint32_t m, size_t bucket_bytes, TileScratch *sc,
 
 // the super-tile cursors of the two-level build (zero between builds)
 uint32_t *super_cursors(Workspace &w) { return w.zeroed + kCurWords + kMaxTiles; }
+
+// The pipelined two-level build's extras: the aux stream (priority: 0 normal, 1
+// high) and its events, and a second zeroed block (spill flags, super cursors and
+// spill bitmap of the odd passes; its fine cursors are unused) plus second pass-1
+// buckets.  Zeroed on the workspace's stream, as ws_reserve does.
+int ws_reserve_alt(Workspace &w, uint32_t m, size_t bucket_bytes, int prio) {
+    const size_t spill_words32 = 2 * (((size_t)m + 63) / 64);
+    const size_t zb = (kCurWords + kMaxTiles + kSuperCurWords + spill_words32) * 4;
+    if (w.aux && w.aux_prio != prio) {
+        NB_HIP(hipStreamSynchronize(w.aux));
+        NB_HIP(hipStreamDestroy(w.aux));
+        w.aux = nullptr;
+    }
+    if (!w.aux) {
+        int lo = 0, hi = 0;
+        NB_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        NB_HIP(hipStreamCreateWithPriority(&w.aux, hipStreamNonBlocking, prio ? hi : lo));
+        w.aux_prio = prio;
+        for (hipEvent_t *e : {&w.ev_bin[0], &w.ev_bin[1], &w.ev_done[0], &w.ev_done[1], &w.ev_start})
+            if (!*e) NB_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
+    if (zb > w.zeroed_alt_bytes || bucket_bytes > w.bucket_alt_bytes) NB_HIP(hipStreamSynchronize(w.st));
+    if (zb > w.zeroed_alt_bytes) {
+        if (w.zeroed_alt) NB_HIP(hipFree(w.zeroed_alt));
+        w.zeroed_alt = nullptr;
+        w.zeroed_alt_bytes = 0;
+        NB_HIP(hipMalloc(&w.zeroed_alt, zb));
+        NB_HIP(hipMemsetAsync(w.zeroed_alt, 0, zb, w.st));
+        w.zeroed_alt_bytes = zb;
+    }
+    return grow(w, &w.buckets_alt, &w.bucket_alt_bytes, bucket_bytes);
+}
 
 using nb::knob;  // the A/B switches (nb_knobs.h): read once, atomics
 
@@ -1769,6 +1810,41 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         return rc;
     const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
     ENTRY *bk = reinterpret_cast<ENTRY *>(ws->buckets);
+    const uint64_t ov = knob(nb::kKnobOverlap);
+    if (ov && n > chunk) {
+        // Pipelined passes (as in launch_two_level): pass p's tile kernel on the aux
+        // stream beside pass p+1's bin kernel; parity q selects the buckets, cursors
+        // and spill scratch.
+        if ((rc = ws_reserve_alt(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * sizeof(ENTRY),
+                                 ov >= 2 ? 1 : 0)))
+            return rc;
+        TileScratch sq[2] = {sc, sc};
+        sq[1].gcur = ws->zeroed_alt;
+        sq[1].spill_flag = ws->zeroed_alt + kCurWords;
+        sq[1].spill32 = ws->zeroed_alt + kCurWords + kMaxTiles + kSuperCurWords;
+        ENTRY *bq[2] = {bk, reinterpret_cast<ENTRY *>(ws->buckets_alt)};
+        NB_HIP(hipEventRecord(ws->ev_start, st));
+        NB_HIP(hipStreamWaitEvent(ws->aux, ws->ev_start, 0));
+        uint64_t pass = 0;
+        for (uint64_t done = 0; done < n; done += chunk, ++pass) {
+            const uint32_t q = pass & 1;
+            const uint64_t cn = std::min(chunk, n - done);
+            const uint8_t *ck = offsets ? keys : keys + done * key_len;
+            const uint64_t *co = offsets ? offsets + done : nullptr;
+            if (pass >= 2) NB_HIP(hipStreamWaitEvent(st, ws->ev_done[q], 0));
+            hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st, ck,
+                               co, key_len, cn, c, tc, sq[q], bq[q]);
+            NB_HIP(hipGetLastError());
+            NB_HIP(hipEventRecord(ws->ev_bin[q], st));
+            NB_HIP(hipStreamWaitEvent(ws->aux, ws->ev_bin[q], 0));
+            hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(tc.T),
+                               dim3(kTileThreads), tile_lds, ws->aux, tc, sq[q], bq[q], words, nwords);
+            NB_HIP(hipGetLastError());
+            NB_HIP(hipEventRecord(ws->ev_done[q], ws->aux));
+        }
+        NB_HIP(hipStreamWaitEvent(st, ws->ev_done[(pass - 1) & 1], 0));
+        return NB_OK;
+    }
     for (uint64_t done = 0; done < n; done += chunk) {
         const uint64_t cn = std::min(chunk, n - done);
         const uint8_t *ck = offsets ? keys : keys + done * key_len;
@@ -1852,6 +1928,50 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
     const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
     E1 *b1 = reinterpret_cast<E1 *>(ws->buckets);
     void *b2 = ws->buckets2;
+    const uint64_t ov = knob(nb::kKnobOverlap);
+    if (ov && n > chunk) {
+        // Pipelined passes: pass p's bin kernel (VALU-bound) on the build stream,
+        // its re-bin and tile kernels (HBM-bound) on the aux stream, so that pass
+        // p's re-bin + tile run beside pass p+1's bin kernel.  Pass parity q selects
+        // the pass-1 buckets, super-tile cursors and spill scratch (the bin kernel of
+        // pass p+2 waits for pass p's tile kernel, the last user of parity q); the
+        // fine buckets and cursors are used on the aux stream only, in pass order.
+        if ((rc = ws_reserve_alt(*ws, c.fm.m, (size_t)t1.T * t1.G * t1.cap * sizeof(E1),
+                                 ov >= 2 ? 1 : 0)))
+            return rc;
+        TileScratch s1[2] = {sc1, sc1}, s2[2] = {sc, sc};
+        s1[1].gcur = ws->zeroed_alt + kCurWords + kMaxTiles;
+        s1[1].spill_flag = s2[1].spill_flag = ws->zeroed_alt + kCurWords;
+        s1[1].spill32 = s2[1].spill32 = ws->zeroed_alt + kCurWords + kMaxTiles + kSuperCurWords;
+        E1 *b1q[2] = {b1, reinterpret_cast<E1 *>(ws->buckets_alt)};
+        // the aux stream starts after everything enqueued on the build stream so far
+        NB_HIP(hipEventRecord(ws->ev_start, st));
+        NB_HIP(hipStreamWaitEvent(ws->aux, ws->ev_start, 0));
+        uint64_t pass = 0;
+        for (uint64_t done = 0; done < n; done += chunk, ++pass) {
+            const uint32_t q = pass & 1;
+            const uint64_t cn = std::min(chunk, n - done);
+            const uint8_t *ck = offsets ? keys : keys + done * key_len;
+            const uint64_t *co = offsets ? offsets + done : nullptr;
+            if (pass >= 2) NB_HIP(hipStreamWaitEvent(st, ws->ev_done[q], 0));
+            hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st, ck,
+                               co, key_len, cn, c, t1, s1[q], b1q[q]);
+            NB_HIP(hipGetLastError());
+            NB_HIP(hipEventRecord(ws->ev_bin[q], st));
+            NB_HIP(hipStreamWaitEvent(ws->aux, ws->ev_bin[q], 0));
+            hipLaunchKernelGGL(rebin, dim3(rebin_x, t1.T), dim3(kRebinThreads), rebin_lds,
+                               ws->aux, t1, t2p, s1[q], s2[q], (const void *)b1q[q], b2);
+            NB_HIP(hipGetLastError());
+            NB_HIP(hipMemsetAsync(s1[q].gcur, 0, (size_t)t1.G * t1.T * 4, ws->aux));
+            hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(t2.T),
+                               dim3(kTileThreads), tile_lds, ws->aux, t2p, s2[q], b2, words, nwords);
+            NB_HIP(hipGetLastError());
+            NB_HIP(hipEventRecord(ws->ev_done[q], ws->aux));
+        }
+        // the build stream joins: the filter is complete when its next work runs
+        NB_HIP(hipStreamWaitEvent(st, ws->ev_done[(pass - 1) & 1], 0));
+        return NB_OK;
+    }
     for (uint64_t done = 0; done < n; done += chunk) {
         const uint64_t cn = std::min(chunk, n - done);
         const uint8_t *ck = offsets ? keys : keys + done * key_len;
@@ -2295,6 +2415,14 @@ int nb_shutdown(void) {
             if (w->zeroed) (void)hipFree(w->zeroed);
             if (w->buckets) (void)hipFree(w->buckets);
             if (w->buckets2) (void)hipFree(w->buckets2);
+            if (w->aux) {
+                (void)hipStreamSynchronize(w->aux);
+                (void)hipStreamDestroy(w->aux);
+            }
+            for (hipEvent_t e : {w->ev_bin[0], w->ev_bin[1], w->ev_done[0], w->ev_done[1], w->ev_start})
+                if (e) (void)hipEventDestroy(e);
+            if (w->zeroed_alt) (void)hipFree(w->zeroed_alt);
+            if (w->buckets_alt) (void)hipFree(w->buckets_alt);
             if (w->probe_hits) (void)hipFree(w->probe_hits);
             if (w->probe_hits_host) (void)hipHostFree(w->probe_hits_host);
             delete w;

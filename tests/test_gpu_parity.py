@@ -457,6 +457,71 @@ def test_two_level_overflow_spill(dev, oracle, knobs):
     np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("overlap", ["1", "2"])
+def test_two_level_overlap(dev, oracle, overlap, knobs):
+    """NB_OVERLAP: the two-level passes pipelined over two streams (pass p's re-bin
+    and tile kernels beside pass p+1's bin kernel, pass-parity scratch).  Odd and
+    even pass counts, overwrite over stale words, duplicated keys spilling in every
+    pass, and an exact normal build afterwards (scratch left clean)."""
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    knobs(NB_BUILD_PATH="tiled", NB_OVERLAP=overlap)
+    m, k = 2**32 - 1, 10
+    n = 700_001
+    buf = synth.fixed_keys(n, 32, seed=91)
+    want = oracle.build(0, buf, None, 32, n, m, k, SEED)
+    for chunk in ("150000", "240000", "350001"):  # 5, 3 and 2 passes
+        knobs(NB_CHUNK_KEYS=chunk)
+        words = torch.full((nbm.nwords(m),), -1, dtype=torch.int64, device=dev)
+        nbm.build_device(t_u8(buf, dev), None, 32, n, m, k, SEED, 0, words, overwrite=True)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(words.cpu().numpy().view(np.uint64), want)
+    dup = np.zeros(400_000 * 32 + 16, np.uint8)
+    dup[: 32 * 5000] = synth.fixed_keys(5000, 32)[: 32 * 5000]
+    knobs(NB_CHUNK_KEYS="90000")
+    got = dev_build(dev, dup, None, 32, 400_000, m, k, SEED)
+    np.testing.assert_array_equal(got, oracle.build(0, dup, None, 32, 400_000, m, k, SEED))
+    vb, vo = synth.var_keys(300_000)
+    got = dev_build(dev, vb, vo, 0, 300_000, m, k, SEED)
+    np.testing.assert_array_equal(got, oracle.build(0, vb, vo, 0, 300_000, m, k, SEED))
+    knobs(NB_OVERLAP="0")
+    got = dev_build(dev, buf, None, 32, n, m, k, SEED)
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("overlap", ["1", "2"])
+def test_tiled_overlap(dev, oracle, overlap, knobs):
+    """NB_OVERLAP on the single-level tiled build: pass p's tile kernel on the aux
+    stream beside pass p+1's bin kernel (packed, u32 and u16 entries; overwrite over
+    stale words; duplicated keys spilling in every pass)."""
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    knobs(NB_BUILD_PATH="tiled", NB_OVERLAP=overlap)
+    fixed = synth.fixed_keys(700_001, 16, seed=5)
+    vb, vo = synth.var_keys(500_000)
+    for m in (958_505_838, 95_850_584, 9_585_059):
+        want = oracle.build(0, fixed, None, 16, 700_001, m, 7, SEED)
+        for chunk in ("100000", "350001"):
+            knobs(NB_CHUNK_KEYS=chunk)
+            words = torch.full((nbm.nwords(m),), -1, dtype=torch.int64, device=dev)
+            nbm.build_device(t_u8(fixed, dev), None, 16, 700_001, m, 7, SEED, 0, words, overwrite=True)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(words.cpu().numpy().view(np.uint64), want)
+        knobs(NB_CHUNK_KEYS="120000")
+        got = dev_build(dev, vb, vo, 0, 500_000, m, 7, SEED)
+        np.testing.assert_array_equal(got, oracle.build(0, vb, vo, 0, 500_000, m, 7, SEED))
+    dup = np.zeros(300_000 * 16 + 16, np.uint8)
+    dup[: 16 * 500] = synth.fixed_keys(500, 16)[: 16 * 500]
+    knobs(NB_CHUNK_KEYS="70000")
+    got = dev_build(dev, dup, None, 16, 300_000, 958_505_838, 7, SEED)
+    np.testing.assert_array_equal(got, oracle.build(0, dup, None, 16, 300_000, 958_505_838, 7, SEED))
+    knobs(NB_OVERLAP="0")
+    got = dev_build(dev, fixed, None, 16, 700_001, 958_505_838, 7, SEED)
+    np.testing.assert_array_equal(got, oracle.build(0, fixed, None, 16, 700_001, 958_505_838, 7, SEED))
+
+
 @pytest.mark.parametrize("chunk", ["4096", "100000", "999999"])
 def test_tiled_chunking(dev, oracle, chunk, knobs):
     from nasp_bloom import synth
