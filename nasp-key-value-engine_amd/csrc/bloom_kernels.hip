@@ -354,6 +354,7 @@ constexpr size_t stage_lds_bytes(int nt) {
     return kStageBytes + (2 * (size_t)nt + kLenClasses) * 4 + 2 * kInitLens * 8;
 }
 constexpr uint32_t kMaxTiles = 4096;
+constexpr uint32_t kMaxCurTiles = 8192;  // cursor / spill-flag slots (two-level fine tiles)
 
 // Diagnostic builds (tools/ubench_tiled.hip) stop a kernel after a phase to price
 // it; in the product this is compiled out.
@@ -1587,12 +1588,15 @@ struct Workspace {
     void *buckets2 = nullptr;     // fine buckets of the two-level build
     size_t bucket2_bytes = 0;
     uint32_t *probe_hits = nullptr;       // the auto probe's sample counts (ProbeGate)
-    uint32_t *probe_hits_host = nullptr;  // pinned copy of them
+    uint32_t *probe_hits_host = nullptr;  // host-mapped coherent words the sample writes
+    uint32_t *probe_hits_map = nullptr;   // ... their device address
+    hipEvent_t ev_probe = nullptr;        // recorded after the sample
     // pipelined two-level passes (NB_OVERLAP): a second stream for the re-bin + tile
     // kernels, the odd passes' pass-1 buckets, super-tile cursors and spill scratch
     hipStream_t aux = nullptr;
     int aux_prio = 0;
-    hipEvent_t ev_bin[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr}, ev_start = nullptr;
+    hipEvent_t ev_bin[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+    hipEvent_t ev_tile[2] = {nullptr, nullptr}, ev_start = nullptr;
     uint32_t *zeroed_alt = nullptr;
     size_t zeroed_alt_bytes = 0;
     void *buckets_alt = nullptr;
@@ -1615,7 +1619,8 @@ int get_ws(hipStream_t st, Workspace **out) {
     return NB_OK;
 }
 
-constexpr size_t kCurWords = (size_t)kShards * kMaxTiles;
+constexpr size_t kCurWords = (size_t)kShards * kMaxCurTiles;
+constexpr size_t kFlagWords = kMaxCurTiles;
 
 // Grows the workspace (synchronising the stream before freeing old buffers).
 // Not graph-capturable when it has to grow: call once with the largest shape first.
@@ -1637,7 +1642,7 @@ constexpr size_t kSuperCurWords = (size_t)kShards * kMaxSuper;
 int ws_reserve(Workspace &w, uint32_t m, size_t bucket_bytes, TileScratch *sc,
                size_t bucket2_bytes = 0) {
     const size_t spill_words32 = 2 * (((size_t)m + 63) / 64);
-    const size_t zb = (kCurWords + kMaxTiles + kSuperCurWords + spill_words32) * 4;
+    const size_t zb = (kCurWords + kFlagWords + kSuperCurWords + spill_words32) * 4;
     if (zb > w.zeroed_bytes || bucket_bytes > w.bucket_bytes || bucket2_bytes > w.bucket2_bytes)
         NB_HIP(hipStreamSynchronize(w.st));
     if (zb > w.zeroed_bytes) {
@@ -1657,12 +1662,12 @@ int ws_reserve(Workspace &w, uint32_t m, size_t bucket_bytes, TileScratch *sc,
         return rc;
     sc->gcur = w.zeroed;
     sc->spill_flag = w.zeroed + kCurWords;
-    sc->spill32 = w.zeroed + kCurWords + kMaxTiles + kSuperCurWords;
+    sc->spill32 = w.zeroed + kCurWords + kFlagWords + kSuperCurWords;
     return NB_OK;
 }
 
 // the super-tile cursors of the two-level build (zero between builds)
-uint32_t *super_cursors(Workspace &w) { return w.zeroed + kCurWords + kMaxTiles; }
+uint32_t *super_cursors(Workspace &w) { return w.zeroed + kCurWords + kFlagWords; }
 
 // The pipelined two-level build's extras: the aux stream (priority: 0 normal, 1
 // high) and its events, and a second zeroed block (spill flags, super cursors and
@@ -1670,7 +1675,7 @@ uint32_t *super_cursors(Workspace &w) { return w.zeroed + kCurWords + kMaxTiles;
 // buckets.  Zeroed on the workspace's stream, as ws_reserve does.
 int ws_reserve_alt(Workspace &w, uint32_t m, size_t bucket_bytes, int prio) {
     const size_t spill_words32 = 2 * (((size_t)m + 63) / 64);
-    const size_t zb = (kCurWords + kMaxTiles + kSuperCurWords + spill_words32) * 4;
+    const size_t zb = (kCurWords + kFlagWords + kSuperCurWords + spill_words32) * 4;
     if (w.aux && w.aux_prio != prio) {
         NB_HIP(hipStreamSynchronize(w.aux));
         NB_HIP(hipStreamDestroy(w.aux));
@@ -1681,7 +1686,8 @@ int ws_reserve_alt(Workspace &w, uint32_t m, size_t bucket_bytes, int prio) {
         NB_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
         NB_HIP(hipStreamCreateWithPriority(&w.aux, hipStreamNonBlocking, prio ? hi : lo));
         w.aux_prio = prio;
-        for (hipEvent_t *e : {&w.ev_bin[0], &w.ev_bin[1], &w.ev_done[0], &w.ev_done[1], &w.ev_start})
+        for (hipEvent_t *e : {&w.ev_bin[0], &w.ev_bin[1], &w.ev_done[0], &w.ev_done[1],
+                              &w.ev_tile[0], &w.ev_tile[1], &w.ev_start})
             if (!*e) NB_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
     if (zb > w.zeroed_alt_bytes || bucket_bytes > w.bucket_alt_bytes) NB_HIP(hipStreamSynchronize(w.st));
@@ -1733,6 +1739,18 @@ TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     cap = (cap + 7) & ~7ull;
     tc.cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFC0ull);
     tc.fts = ts;
+    return tc;
+}
+
+// The same tiling at a given tile size (NB_FINE_BITS: the two-level build's fine tiles).
+TileCfg retile(const TileCfg &base, uint32_t m, uint64_t n_chunk, uint32_t k, uint32_t ts) {
+    TileCfg tc = base;
+    tc.ts = tc.fts = ts;
+    tc.T = (uint32_t)(((uint64_t)m + (1ull << ts) - 1) >> ts);
+    const double e = (double)n_chunk * k / ((double)tc.T * tc.G);
+    uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
+    cap = (cap + 7) & ~7ull;
+    tc.cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFC0ull);
     return tc;
 }
 
@@ -1810,41 +1828,6 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         return rc;
     const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
     ENTRY *bk = reinterpret_cast<ENTRY *>(ws->buckets);
-    const uint64_t ov = knob(nb::kKnobOverlap);
-    if (ov && n > chunk) {
-        // Pipelined passes (as in launch_two_level): pass p's tile kernel on the aux
-        // stream beside pass p+1's bin kernel; parity q selects the buckets, cursors
-        // and spill scratch.
-        if ((rc = ws_reserve_alt(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * sizeof(ENTRY),
-                                 ov >= 2 ? 1 : 0)))
-            return rc;
-        TileScratch sq[2] = {sc, sc};
-        sq[1].gcur = ws->zeroed_alt;
-        sq[1].spill_flag = ws->zeroed_alt + kCurWords;
-        sq[1].spill32 = ws->zeroed_alt + kCurWords + kMaxTiles + kSuperCurWords;
-        ENTRY *bq[2] = {bk, reinterpret_cast<ENTRY *>(ws->buckets_alt)};
-        NB_HIP(hipEventRecord(ws->ev_start, st));
-        NB_HIP(hipStreamWaitEvent(ws->aux, ws->ev_start, 0));
-        uint64_t pass = 0;
-        for (uint64_t done = 0; done < n; done += chunk, ++pass) {
-            const uint32_t q = pass & 1;
-            const uint64_t cn = std::min(chunk, n - done);
-            const uint8_t *ck = offsets ? keys : keys + done * key_len;
-            const uint64_t *co = offsets ? offsets + done : nullptr;
-            if (pass >= 2) NB_HIP(hipStreamWaitEvent(st, ws->ev_done[q], 0));
-            hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st, ck,
-                               co, key_len, cn, c, tc, sq[q], bq[q]);
-            NB_HIP(hipGetLastError());
-            NB_HIP(hipEventRecord(ws->ev_bin[q], st));
-            NB_HIP(hipStreamWaitEvent(ws->aux, ws->ev_bin[q], 0));
-            hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(tc.T),
-                               dim3(kTileThreads), tile_lds, ws->aux, tc, sq[q], bq[q], words, nwords);
-            NB_HIP(hipGetLastError());
-            NB_HIP(hipEventRecord(ws->ev_done[q], ws->aux));
-        }
-        NB_HIP(hipStreamWaitEvent(st, ws->ev_done[(pass - 1) & 1], 0));
-        return NB_OK;
-    }
     for (uint64_t done = 0; done < n; done += chunk) {
         const uint64_t cn = std::min(chunk, n - done);
         const uint8_t *ck = offsets ? keys : keys + done * key_len;
@@ -1870,9 +1853,28 @@ void (*tile_kernel_of())(TileCfg, TileScratch, const void *, uint64_t *, uint64_
 // tail; NB_PACK5=0 for the A/B) or 32-bit indices.
 bool two_level_pack5() { return knob(nb::kKnobPack5) != 0; }
 
-// The two-level build (see bloom_rebin_kernel): per chunk, the bin kernel into
-// super tiles, the re-bin into fine tiles, the tile kernel on the fine tiles.
-// E1: pass-1 entry type (Pack5 or uint32_t); t1 comes with its capacity in entries.
+// Bucket capacity (entries) of one (tile, shard) for n keys: mean + 8 sigma + 64.
+uint32_t cap_for(uint32_t T, uint32_t G, uint64_t n, uint32_t k) {
+    const double e = (double)n * k / ((double)T * G);
+    uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
+    cap = (cap + 7) & ~7ull;
+    return (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFC0ull);
+}
+
+// The two-level build (see bloom_rebin_kernel): per pass (`chunk` keys), the bin
+// kernel into super tiles and the re-bin into fine tiles for each of its
+// NB_SUBPASSES sub-passes (the fine buckets accumulate), then the tile kernel on the
+// fine tiles.  E1: pass-1 entry type (Pack5 or uint32_t); t2 comes with its capacity
+// in entries for `chunk` keys.
+//
+// NB_OVERLAP: the sub-passes pipelined over two streams -- every bin kernel
+// (VALU-bound) on the build stream, every re-bin and tile kernel (HBM-bound) on the
+// workspace's aux stream, so that sub-pass s's re-bin runs beside sub-pass s+1's
+// bin kernel (a re-bin block fits a CU beside a bin block; a 128 KB tile block does
+// not, so a pass's first bin kernel waits for the previous pass's tile kernel unless
+// NB_OVERLAP & 4).  Sub-pass parity selects the pass-1 buckets and super-tile
+// cursors, pass parity the spill scratch; the fine buckets and cursors are used on
+// the aux stream only, in order.  NB_OVERLAP & 3 == 2: the aux stream at high priority.
 template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR, int KX, typename E1>
 int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                      const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st,
@@ -1884,10 +1886,14 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
     int rc;
     if ((rc = get_ws(st, &ws))) return rc;
     std::lock_guard<std::mutex> lk(ws->mu);
+    const uint64_t nsub = std::max<uint64_t>(1, std::min<uint64_t>(knob(nb::kKnobSubpasses), 64));
+    const uint64_t sub = std::min<uint64_t>(chunk, ((chunk + nsub - 1) / nsub + kpb - 1) / kpb * kpb);
+    const uint64_t spp = (chunk + sub - 1) / sub;  // sub-passes per pass
     // pass-1 capacity in units: the entries' plus <= 4 pad slots per bin block of
     // the shard, / 5
-    const uint64_t nblk = (chunk + kpb - 1) / kpb;
+    const uint64_t nblk = (sub + kpb - 1) / kpb;
     TileCfg t1 = t1e;
+    t1.cap = cap_for(t1.T, t1.G, sub, c.k);
     if (IN5) {
         const uint64_t bps = (nblk + t1.G - 1) / t1.G;
         const uint64_t capu = ((uint64_t)t1.cap + 4 * bps + 4) / 5;
@@ -1896,20 +1902,20 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
     const uint32_t span_units = kRebinThreads * (IN5 ? rebin_ept<true>() / 5 : rebin_ept<false>());
     const uint32_t rebin_x = (uint32_t)(((uint64_t)t1.cap * t1.G + span_units - 1) / span_units);
     // fine entries packed three per word (2^ts2 <= 2^21): capacity in words, the
-    // entries' plus <= 2 pad slots per re-bin block of the shard
+    // entries' plus <= 2 pad slots per re-bin block of the shard (every sub-pass's)
     const bool pack = t2.ts <= 20 && knob(nb::kKnobPack) != 0;
     TileCfg t2p = t2;
     if (pack) {
-        const uint64_t bps = ((uint64_t)rebin_x + t2.G - 1) / t2.G;
+        const uint64_t bps = ((uint64_t)rebin_x * spp + t2.G - 1) / t2.G;
         const uint64_t capw = ((uint64_t)t2.cap + 2 * bps + 2) / 3;
         t2p.cap = (uint32_t)std::min<uint64_t>((capw + 7) & ~7ull, 0xFFFFFFC0ull);
     }
     const size_t e2 = pack ? 8 : 4;
-    if ((rc = ws_reserve(*ws, c.fm.m, (size_t)t1.T * t1.G * t1.cap * sizeof(E1), &sc,
-                         (size_t)t2p.T * t2p.G * t2p.cap * e2)))
+    const size_t b1_bytes = (size_t)t1.T * t1.G * t1.cap * sizeof(E1);
+    if ((rc = ws_reserve(*ws, c.fm.m, b1_bytes, &sc, (size_t)t2p.T * t2p.G * t2p.cap * e2)))
         return rc;
-    TileScratch sc1 = sc;
-    sc1.gcur = super_cursors(*ws);
+    const uint64_t ov = n > sub ? knob(nb::kKnobOverlap) : 0;
+    if (ov && (rc = ws_reserve_alt(*ws, c.fm.m, b1_bytes, (ov & 3) >= 2 ? 1 : 0))) return rc;
     size_t sort_bytes = kpb * c.k * 4;
     if (IN5) sort_bytes += (size_t)t1.T * 16;  // <= 4 pad slots per run
     if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(NT));
@@ -1926,67 +1932,62 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
     NB_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(rebin),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)rebin_lds));
     const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
-    E1 *b1 = reinterpret_cast<E1 *>(ws->buckets);
-    void *b2 = ws->buckets2;
-    const uint64_t ov = knob(nb::kKnobOverlap);
-    if (ov && n > chunk) {
-        // Pipelined passes: pass p's bin kernel (VALU-bound) on the build stream,
-        // its re-bin and tile kernels (HBM-bound) on the aux stream, so that pass
-        // p's re-bin + tile run beside pass p+1's bin kernel.  Pass parity q selects
-        // the pass-1 buckets, super-tile cursors and spill scratch (the bin kernel of
-        // pass p+2 waits for pass p's tile kernel, the last user of parity q); the
-        // fine buckets and cursors are used on the aux stream only, in pass order.
-        if ((rc = ws_reserve_alt(*ws, c.fm.m, (size_t)t1.T * t1.G * t1.cap * sizeof(E1),
-                                 ov >= 2 ? 1 : 0)))
-            return rc;
-        TileScratch s1[2] = {sc1, sc1}, s2[2] = {sc, sc};
-        s1[1].gcur = ws->zeroed_alt + kCurWords + kMaxTiles;
-        s1[1].spill_flag = s2[1].spill_flag = ws->zeroed_alt + kCurWords;
-        s1[1].spill32 = s2[1].spill32 = ws->zeroed_alt + kCurWords + kMaxTiles + kSuperCurWords;
-        E1 *b1q[2] = {b1, reinterpret_cast<E1 *>(ws->buckets_alt)};
+    // scratch by parity: [0] the workspace's, [1] the alt block's (NB_OVERLAP only)
+    TileScratch fine[2] = {sc, sc}, super[2] = {sc, sc};
+    super[0].gcur = super[1].gcur = super_cursors(*ws);
+    E1 *b1q[2] = {reinterpret_cast<E1 *>(ws->buckets), reinterpret_cast<E1 *>(ws->buckets)};
+    if (ov) {
+        fine[1].spill_flag = super[1].spill_flag = ws->zeroed_alt + kCurWords;
+        fine[1].spill32 = super[1].spill32 = ws->zeroed_alt + kCurWords + kFlagWords + kSuperCurWords;
+        super[1].gcur = ws->zeroed_alt + kCurWords + kFlagWords;
+        b1q[1] = reinterpret_cast<E1 *>(ws->buckets_alt);
         // the aux stream starts after everything enqueued on the build stream so far
         NB_HIP(hipEventRecord(ws->ev_start, st));
         NB_HIP(hipStreamWaitEvent(ws->aux, ws->ev_start, 0));
-        uint64_t pass = 0;
-        for (uint64_t done = 0; done < n; done += chunk, ++pass) {
-            const uint32_t q = pass & 1;
-            const uint64_t cn = std::min(chunk, n - done);
+    }
+    hipStream_t sa = ov ? ws->aux : st;  // re-bin + tile stream
+    void *b2 = ws->buckets2;
+    uint64_t s_i = 0, pass = 0;
+    for (uint64_t pdone = 0; pdone < n; pdone += chunk, ++pass) {
+        const uint64_t pend = std::min(n, pdone + chunk);
+        const uint32_t r = ov ? pass & 1 : 0;  // spill scratch of this pass
+        for (uint64_t done = pdone; done < pend; done += sub, ++s_i) {
+            const uint32_t q = ov ? s_i & 1 : 0;  // pass-1 buckets + super cursors
+            const uint64_t cn = std::min(sub, pend - done);
             const uint8_t *ck = offsets ? keys : keys + done * key_len;
             const uint64_t *co = offsets ? offsets + done : nullptr;
-            if (pass >= 2) NB_HIP(hipStreamWaitEvent(st, ws->ev_done[q], 0));
-            hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st, ck,
-                               co, key_len, cn, c, t1, s1[q], b1q[q]);
+            TileScratch s1 = super[q];
+            s1.spill_flag = fine[r].spill_flag;
+            s1.spill32 = fine[r].spill32;
+            if (ov) {
+                // b1q[q] and super[q] are free once sub-pass s_i - 2's re-bin (and the
+                // cursor reset behind it) is done; the spill scratch r once pass - 2's
+                // tile kernel is; and the tile kernel enqueued last is waited for
+                if (s_i >= 2) NB_HIP(hipStreamWaitEvent(st, ws->ev_done[q], 0));
+                if (pass >= 2 && done == pdone) NB_HIP(hipStreamWaitEvent(st, ws->ev_tile[r], 0));
+                if (pass >= 1 && done == pdone && !(ov & 4))  // (NB_OVERLAP & 4: no wait)
+                    NB_HIP(hipStreamWaitEvent(st, ws->ev_tile[r ^ 1], 0));
+            }
+            hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st,
+                               ck, co, key_len, cn, c, t1, s1, b1q[q]);
             NB_HIP(hipGetLastError());
-            NB_HIP(hipEventRecord(ws->ev_bin[q], st));
-            NB_HIP(hipStreamWaitEvent(ws->aux, ws->ev_bin[q], 0));
-            hipLaunchKernelGGL(rebin, dim3(rebin_x, t1.T), dim3(kRebinThreads), rebin_lds,
-                               ws->aux, t1, t2p, s1[q], s2[q], (const void *)b1q[q], b2);
+            if (ov) {
+                NB_HIP(hipEventRecord(ws->ev_bin[q], st));
+                NB_HIP(hipStreamWaitEvent(sa, ws->ev_bin[q], 0));
+            }
+            hipLaunchKernelGGL(rebin, dim3(rebin_x, t1.T), dim3(kRebinThreads), rebin_lds, sa, t1,
+                               t2p, s1, fine[r], (const void *)b1q[q], b2);
             NB_HIP(hipGetLastError());
-            NB_HIP(hipMemsetAsync(s1[q].gcur, 0, (size_t)t1.G * t1.T * 4, ws->aux));
-            hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(t2.T),
-                               dim3(kTileThreads), tile_lds, ws->aux, t2p, s2[q], b2, words, nwords);
-            NB_HIP(hipGetLastError());
-            NB_HIP(hipEventRecord(ws->ev_done[q], ws->aux));
+            NB_HIP(hipMemsetAsync(s1.gcur, 0, (size_t)t1.G * t1.T * 4, sa));  // keep them zero
+            if (ov) NB_HIP(hipEventRecord(ws->ev_done[q], sa));
         }
-        // the build stream joins: the filter is complete when its next work runs
-        NB_HIP(hipStreamWaitEvent(st, ws->ev_done[(pass - 1) & 1], 0));
-        return NB_OK;
+        hipLaunchKernelGGL((overwrite && pdone == 0) ? tile_ow : tile_or, dim3(t2.T),
+                           dim3(kTileThreads), tile_lds, sa, t2p, fine[r], b2, words, nwords);
+        NB_HIP(hipGetLastError());
+        if (ov) NB_HIP(hipEventRecord(ws->ev_tile[r], sa));
     }
-    for (uint64_t done = 0; done < n; done += chunk) {
-        const uint64_t cn = std::min(chunk, n - done);
-        const uint8_t *ck = offsets ? keys : keys + done * key_len;
-        const uint64_t *co = offsets ? offsets + done : nullptr;
-        hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st, ck,
-                           co, key_len, cn, c, t1, sc1, b1);
-        NB_HIP(hipGetLastError());
-        hipLaunchKernelGGL(rebin, dim3(rebin_x, t1.T), dim3(kRebinThreads), rebin_lds,
-                           st, t1, t2p, sc1, sc, (const void *)b1, b2);
-        NB_HIP(hipGetLastError());
-        NB_HIP(hipMemsetAsync(sc1.gcur, 0, (size_t)t1.G * t1.T * 4, st));  // keep them zero
-        hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(t2.T),
-                           dim3(kTileThreads), tile_lds, st, t2p, sc, b2, words, nwords);
-        NB_HIP(hipGetLastError());
-    }
+    // the build stream joins: the filter is complete when its next work runs
+    if (ov) NB_HIP(hipStreamWaitEvent(st, ws->ev_tile[(pass - 1) & 1], 0));
     return NB_OK;
 }
 
@@ -2006,6 +2007,16 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
         if (const uint64_t v = knob(nb::kKnobChunkKeys)) chunk = std::min<uint64_t>(n, v);
         tc = choose_tiles(c.fm.m, chunk, c.k);
         if constexpr (KR > 0) {
+            // NB_FINE_BITS = 19: 2^19-bit fine tiles (64 KB of LDS per tile block, so a
+            // tile block fits beside a bin or re-bin block), 64 per 2^25-bit super tile
+            const uint32_t fb = (uint32_t)knob(nb::kKnobFineBits);
+            if (fb == 19 && ((uint64_t)c.fm.m + (1u << 19) - 1) >> 19 <= kMaxCurTiles) {
+                const TileCfg t2 = retile(tc, c.fm.m, chunk, c.k, 19);
+                if (two_level_pack5())
+                    return launch_two_level<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, KX, Pack5>(
+                        keys, offsets, key_len, n, c, words, overwrite, st, chunk,
+                        super_tiles(t2, c.fm.m, chunk, c.k, 6), t2);
+            }
             if (two_level_pack5())  // 2^(ts+5)-bit super tiles: 25-bit offsets
                 return launch_two_level<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, KX, Pack5>(
                     keys, offsets, key_len, n, c, words, overwrite, st, chunk,
@@ -2232,25 +2243,33 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     {
         std::lock_guard<std::mutex> lk(ws->mu);
         if (!ws->probe_hits) NB_HIP(hipMalloc(&ws->probe_hits, kProbeSampleBlocks * 4));
-        if (!ws->probe_hits_host)
-            NB_HIP(hipHostMalloc(&ws->probe_hits_host, kProbeSampleBlocks * 4, hipHostMallocDefault));
+        if (!ws->probe_hits_host) {
+            NB_HIP(hipHostMalloc(&ws->probe_hits_host, kProbeSampleBlocks * 4,
+                                 hipHostMallocMapped | hipHostMallocCoherent));
+            NB_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&ws->probe_hits_map),
+                                           ws->probe_hits_host, 0));
+        }
+        if (!ws->ev_probe) NB_HIP(hipEventCreateWithFlags(&ws->ev_probe, hipEventDisableTiming));
     }
     const uint64_t S = kProbeSample;
-    const ProbeGate sample{ws->probe_hits, nullptr, kProbeSampleBlocks, (uint32_t)S, 1};
     const uint8_t *rk = offsets ? keys : keys + S * key_len;
     const uint64_t *ro = offsets ? offsets + S : nullptr;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    NB_HIP(hipStreamIsCapturing(st, &cs));
+    // outside capture the sample's blocks write their counts straight into host-mapped
+    // memory (no copy launch); under capture into device words the gated launches read
+    const ProbeGate sample{cs == hipStreamCaptureStatusNone ? ws->probe_hits_map : ws->probe_hits,
+                           nullptr, kProbeSampleBlocks, (uint32_t)S, 1};
     hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, LAYOUT>), dim3(kProbeSampleBlocks), dim3(kBlock), 0,
                        st, keys, offsets, key_len, S, c, reinterpret_cast<const uint32_t *>(words),
                        out, sample);
     NB_HIP(hipGetLastError());
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    NB_HIP(hipStreamIsCapturing(st, &cs));
     if (cs == hipStreamCaptureStatusNone) {
-        NB_HIP(hipMemcpyAsync(ws->probe_hits_host, ws->probe_hits, kProbeSampleBlocks * 4,
-                              hipMemcpyDeviceToHost, st));
-        NB_HIP(hipStreamSynchronize(st));
+        NB_HIP(hipEventRecord(ws->ev_probe, st));
+        NB_HIP(hipEventSynchronize(ws->ev_probe));
         uint64_t h = 0;
-        for (uint32_t b = 0; b < kProbeSampleBlocks; ++b) h += ws->probe_hits_host[b];
+        for (uint32_t b = 0; b < kProbeSampleBlocks; ++b)
+            h += reinterpret_cast<volatile uint32_t *>(ws->probe_hits_host)[b];
         if (2 * h >= S) return tiled(rk, ro, n - S, out + S, none);  // as gate_open decides
         return launch_probe_lane<FLAVOR, LAYOUT>(rk, ro, key_len, n - S, c, words, out + S, st, none);
     }
@@ -2419,12 +2438,14 @@ int nb_shutdown(void) {
                 (void)hipStreamSynchronize(w->aux);
                 (void)hipStreamDestroy(w->aux);
             }
-            for (hipEvent_t e : {w->ev_bin[0], w->ev_bin[1], w->ev_done[0], w->ev_done[1], w->ev_start})
+            for (hipEvent_t e : {w->ev_bin[0], w->ev_bin[1], w->ev_done[0], w->ev_done[1],
+                                 w->ev_tile[0], w->ev_tile[1], w->ev_start})
                 if (e) (void)hipEventDestroy(e);
             if (w->zeroed_alt) (void)hipFree(w->zeroed_alt);
             if (w->buckets_alt) (void)hipFree(w->buckets_alt);
             if (w->probe_hits) (void)hipFree(w->probe_hits);
             if (w->probe_hits_host) (void)hipHostFree(w->probe_hits_host);
+            if (w->ev_probe) (void)hipEventDestroy(w->ev_probe);
             delete w;
         }
         g_ws.clear();

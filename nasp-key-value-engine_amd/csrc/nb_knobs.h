@@ -30,10 +30,13 @@ enum Knob : int {
     kKnobBinWide,       // NB_BIN_WIDE       1: larger bin blocks (2 304 keys for 16-byte keys
                         //                   at k = 7, 1 792 for 32-byte keys at k = 10)
     kKnobShardedStage,  // NB_SHARDED_STAGE  1: nb_build_sharded stages every merge source
-    kKnobOverlap,       // NB_OVERLAP        1: two-level passes pipelined over two streams
-                        //                   (pass p's re-bin + tile kernels beside pass
-                        //                   p+1's bin kernel); 2: the same, the second
+    kKnobOverlap,       // NB_OVERLAP        1: two-level sub-passes pipelined over two
+                        //                   streams (sub-pass s's re-bin beside sub-pass
+                        //                   s+1's bin kernel); 2: the same, the second
                         //                   stream at high priority
+    kKnobSubpasses,     // NB_SUBPASSES      bin + re-bin sub-passes per tile pass (1)
+    kKnobFineBits,      // NB_FINE_BITS      0: fine-tile policy (2^20 bits); 19: 2^19-bit fine
+                        //                   tiles in the two-level build
     kKnobProbePath,     // NB_PROBE_PATH     0 auto | 1 "lane" (one lane per key) | 2 "tiled"
     kKnobFailBuilds,    // NB_FAIL_BUILDS    fault injection: the next N device builds fail
                         //                   with NB_ERR_HIP before launching anything

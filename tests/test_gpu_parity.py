@@ -457,16 +457,19 @@ def test_two_level_overflow_spill(dev, oracle, knobs):
     np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("overlap", ["1", "2"])
-def test_two_level_overlap(dev, oracle, overlap, knobs):
-    """NB_OVERLAP: the two-level passes pipelined over two streams (pass p's re-bin
-    and tile kernels beside pass p+1's bin kernel, pass-parity scratch).  Odd and
-    even pass counts, overwrite over stale words, duplicated keys spilling in every
-    pass, and an exact normal build afterwards (scratch left clean)."""
+@pytest.mark.parametrize("overlap,fine,sub", [("1", "0", "1"), ("2", "0", "2"), ("6", "0", "3"),
+                                              ("0", "0", "3"), ("0", "19", "1"), ("2", "19", "2")])
+def test_two_level_overlap(dev, oracle, overlap, fine, sub, knobs):
+    """NB_OVERLAP: the two-level sub-passes pipelined over two streams (a re-bin
+    beside the next bin kernel; & 4: a tile kernel beside the next pass's bin kernel;
+    sub-pass- and pass-parity scratch); NB_SUBPASSES: bin + re-bin sub-passes sharing
+    one tile pass; NB_FINE_BITS = 19: 8 192 fine tiles of 2^19 bits, 64 per super
+    tile.  Odd and even pass counts, overwrite over stale words, duplicated keys
+    spilling in every pass, and an exact normal build afterwards (scratch clean)."""
     import torch
     import nasp_bloom as nbm
     from nasp_bloom import synth
-    knobs(NB_BUILD_PATH="tiled", NB_OVERLAP=overlap)
+    knobs(NB_BUILD_PATH="tiled", NB_OVERLAP=overlap, NB_FINE_BITS=fine, NB_SUBPASSES=sub)
     m, k = 2**32 - 1, 10
     n = 700_001
     buf = synth.fixed_keys(n, 32, seed=91)
@@ -485,41 +488,9 @@ def test_two_level_overlap(dev, oracle, overlap, knobs):
     vb, vo = synth.var_keys(300_000)
     got = dev_build(dev, vb, vo, 0, 300_000, m, k, SEED)
     np.testing.assert_array_equal(got, oracle.build(0, vb, vo, 0, 300_000, m, k, SEED))
-    knobs(NB_OVERLAP="0")
+    knobs(NB_OVERLAP="0", NB_FINE_BITS="0", NB_SUBPASSES="1")
     got = dev_build(dev, buf, None, 32, n, m, k, SEED)
     np.testing.assert_array_equal(got, want)
-
-
-@pytest.mark.parametrize("overlap", ["1", "2"])
-def test_tiled_overlap(dev, oracle, overlap, knobs):
-    """NB_OVERLAP on the single-level tiled build: pass p's tile kernel on the aux
-    stream beside pass p+1's bin kernel (packed, u32 and u16 entries; overwrite over
-    stale words; duplicated keys spilling in every pass)."""
-    import torch
-    import nasp_bloom as nbm
-    from nasp_bloom import synth
-    knobs(NB_BUILD_PATH="tiled", NB_OVERLAP=overlap)
-    fixed = synth.fixed_keys(700_001, 16, seed=5)
-    vb, vo = synth.var_keys(500_000)
-    for m in (958_505_838, 95_850_584, 9_585_059):
-        want = oracle.build(0, fixed, None, 16, 700_001, m, 7, SEED)
-        for chunk in ("100000", "350001"):
-            knobs(NB_CHUNK_KEYS=chunk)
-            words = torch.full((nbm.nwords(m),), -1, dtype=torch.int64, device=dev)
-            nbm.build_device(t_u8(fixed, dev), None, 16, 700_001, m, 7, SEED, 0, words, overwrite=True)
-            torch.cuda.synchronize()
-            np.testing.assert_array_equal(words.cpu().numpy().view(np.uint64), want)
-        knobs(NB_CHUNK_KEYS="120000")
-        got = dev_build(dev, vb, vo, 0, 500_000, m, 7, SEED)
-        np.testing.assert_array_equal(got, oracle.build(0, vb, vo, 0, 500_000, m, 7, SEED))
-    dup = np.zeros(300_000 * 16 + 16, np.uint8)
-    dup[: 16 * 500] = synth.fixed_keys(500, 16)[: 16 * 500]
-    knobs(NB_CHUNK_KEYS="70000")
-    got = dev_build(dev, dup, None, 16, 300_000, 958_505_838, 7, SEED)
-    np.testing.assert_array_equal(got, oracle.build(0, dup, None, 16, 300_000, 958_505_838, 7, SEED))
-    knobs(NB_OVERLAP="0")
-    got = dev_build(dev, fixed, None, 16, 700_001, 958_505_838, 7, SEED)
-    np.testing.assert_array_equal(got, oracle.build(0, fixed, None, 16, 700_001, 958_505_838, 7, SEED))
 
 
 @pytest.mark.parametrize("chunk", ["4096", "100000", "999999"])

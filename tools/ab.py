@@ -39,10 +39,14 @@ def main():
                 for kv in filter(None, envs.split(",")):
                     k, _, val = kv.partition("=")
                     env[k] = os.path.join(REPO, val) if k == "NB_LIB" else val
-                steps = min(args.steps, 3) if wl == "c5" else args.steps
-                cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--workload", wl,
-                       "--no-cpu-baseline", "--no-host-path", "--no-probe", "--no-c2", "--no-rank-share",
-                       "--steps", str(steps), "--warmup", "1" if wl == "c5" else "3"]
+                steps = min(args.steps, 3) if wl in ("c5", "c5r") else args.steps
+                # c5r: the per-rank share of an 8-GPU C5 step (bench.py per_rank_at_8)
+                cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--workload", wl[:2],
+                       "--no-cpu-baseline", "--no-host-path", "--no-probe", "--no-c2",
+                       "--steps", str(1 if wl == "c5r" else steps),
+                       "--warmup", "1" if wl in ("c5", "c5r") else "3"]
+                if wl != "c5r":
+                    cmd.append("--no-rank-share")
                 r = subprocess.run(cmd, env=env, capture_output=True, text=True,
                                    timeout=args.timeout)
                 if r.returncode != 0:
@@ -52,6 +56,8 @@ def main():
                 open(os.path.join(out_dir, f"ab_{label}_{wl}_{rep}.json"), "w").write(line + "\n")
                 d = json.loads(line)
                 ms = d["roofline"].get("kernel_ms", d["ms_per_step"])  # c5: whole step
+                if wl == "c5r":
+                    ms = d["per_rank_at_8"]["ms"]
                 table.setdefault((wl, label), []).append(ms)
                 print(f"rep {rep} {wl:3s} {label:14s} {ms:.4f} ms  {d['value']:.0f} Mkeys/s "
                       f"frac {d['roofline']['frac']:.4f}", flush=True)
