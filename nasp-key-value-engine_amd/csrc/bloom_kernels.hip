@@ -378,6 +378,9 @@ constexpr uint32_t kMaxCurTiles = 8192;  // cursor / spill-flag slots (two-level
 // L2 otherwise merges), non-temporal bucket loads in the tile and re-bin kernels
 // (read once; on by default).  Non-temporal key loads in the bin kernel measured
 // 0.5-1 % slower (C3/C4/C5) and are not used.
+#ifndef NB_PACK_HALVES  // packed bucket words built in 32-bit halves (A/B: 0 = 64-bit shifts)
+#define NB_PACK_HALVES 1
+#endif
 #ifndef NB_NT_STORE
 #define NB_NT_STORE 0
 #endif
@@ -637,11 +640,18 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
         return;
     } else if constexpr (PACK) {
         // word q of the block = slots 3q..3q+2 (one run, tile of the first slot)
-        const uint32_t words = total / 3, msk = (1u << tc.ts) - 1;
+        const uint32_t words = total / 3, msk = (1u << tc.ts) - 1, hb = tc.ts - 11;
+        // a | b << 21 | c << 42 (21-bit fields, offsets masked to ts bits), built in
+        // 32-bit halves: lo = a | b[0,11) << 21 (b << 21 drops b's high bits), hi =
+        // b[11,ts) | c << 10 -- 5 VALU instead of the 64-bit shifts' 7-8 (17 <= ts <= 20)
         auto word_at = [&](uint32_t q, uint32_t *t) {
             const uint32_t a = sorted[3 * q], b = sorted[3 * q + 1], c = sorted[3 * q + 2];
             *t = a >> tc.ts;
-            return (uint64_t)(a & msk) | ((uint64_t)(b & msk) << 21) | ((uint64_t)(c & msk) << 42);
+            if (!NB_PACK_HALVES)
+                return (uint64_t)(a & msk) | ((uint64_t)(b & msk) << 21) | ((uint64_t)(c & msk) << 42);
+            const uint32_t lo = (a & msk) | (b << 21);
+            const uint32_t hi = __builtin_amdgcn_ubfe(b, 11, hb) | ((c & msk) << 10);
+            return (uint64_t)hi << 32 | lo;
         };
         if (!any_ovf && b32) {
             char *bb = reinterpret_cast<char *>(buckets);
@@ -1252,9 +1262,10 @@ __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
         for (uint32_t q = tid; q < words; q += kRebinThreads) {
             const uint32_t a = sorted[3 * q], b = sorted[3 * q + 1], c = sorted[3 * q + 2];
             const uint32_t f = (a >> t2.ts) - fbase;
-            if (!ovf || q < flim[f]) {
-                bw[fGX[f] + q] = (uint64_t)(a & msk) | ((uint64_t)(b & msk) << 21) |
-                                 ((uint64_t)(c & msk) << 42);
+            if (!ovf || q < flim[f]) {  // a | b << 21 | c << 42 in 32-bit halves (as in bin_tail_two_tiles)
+                const uint32_t lo = (a & msk) | (b << 21);
+                const uint32_t hi = __builtin_amdgcn_ubfe(b, 11, t2.ts - 11) | ((c & msk) << 10);
+                bw[fGX[f] + q] = (uint64_t)hi << 32 | lo;
             } else {
                 for (uint32_t rr = 0; rr < 3; ++rr) {
                     const uint32_t x = sorted[3 * q + rr];
