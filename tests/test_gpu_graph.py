@@ -96,3 +96,41 @@ def test_auto_probe_replayed_from_graph(dev, oracle, present):
     got = out.cpu().numpy()
     np.testing.assert_array_equal(got, oracle.probe(0, keys, None, 16, n, m, k, SEED, words_np))
     assert got.all() == present
+
+
+def test_two_level_pipelined_build_replayed_from_graph(dev, oracle, knobs):
+    """The two-level build pipelined over two streams (NB_OVERLAP, the default for
+    T > 2 048 tiles) under stream capture: the aux stream joins the capture through
+    the first event and rejoins the build stream at the end (fork / join), so the
+    captured graph holds every pass's bin, re-bin, cursor reset and tile kernels;
+    replays on new keys give the oracle's filter, bit-exact."""
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    knobs(NB_BUILD_PATH="tiled", NB_CHUNK_KEYS="300000")  # 3 passes x 2 sub-passes
+    assert nbm.get_knob("NB_OVERLAP") != 0
+    n, m, k = 700_001, 2**32 - 1, 10
+    sets = [synth.fixed_keys(n, 32, seed=300 + s) for s in range(2)]
+    kt = torch.zeros(sets[0].size, dtype=torch.uint8, device=dev)
+    words = torch.zeros(nbm.nwords(m), dtype=torch.int64, device=dev)
+    st = torch.cuda.Stream(device=dev)
+
+    def build():
+        nbm.build_device(kt, None, 32, n, m, k, SEED, 0, words, stream=st, overwrite=True)
+
+    kt.copy_(torch.from_numpy(sets[0]))
+    torch.cuda.synchronize()
+    with torch.cuda.stream(st):
+        build()  # warm-up: sizes the workspace, creates the aux stream
+    st.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        build()
+    for i in (1, 0):
+        kt.copy_(torch.from_numpy(sets[i]))
+        words.fill_(-1)  # overwrite mode: stale words must not survive
+        torch.cuda.synchronize()
+        g.replay()
+        torch.cuda.synchronize()
+        want = oracle.build(0, sets[i], None, 32, n, m, k, SEED)
+        np.testing.assert_array_equal(words.cpu().numpy().view(np.uint64), want)
