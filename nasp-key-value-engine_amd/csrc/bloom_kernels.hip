@@ -378,6 +378,9 @@ constexpr uint32_t kMaxCurTiles = 8192;  // cursor / spill-flag slots (two-level
 // L2 otherwise merges), non-temporal bucket loads in the tile and re-bin kernels
 // (read once; on by default).  Non-temporal key loads in the bin kernel measured
 // 0.5-1 % slower (C3/C4/C5) and are not used.
+#ifndef NB_PLACE_BATCH  // bin placement: a key's run-start reads before its stores (A/B: 0)
+#define NB_PLACE_BATCH 1
+#endif
 #ifndef NB_PACK_HALVES  // packed bucket words built in 32-bit halves (A/B: 0 = 64-bit shifts)
 #define NB_PACK_HALVES 1
 #endif
@@ -559,16 +562,45 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     }
     __syncthreads();
     if (NB_DIAG_STOP(2)) return;
-    // ---- phase 3: placement (the reservations' round trips overlap it)
+    // ---- phase 3: placement (the reservations' round trips overlap it).  A key's
+    // run-start reads are all issued before its stores: the compiler cannot tell a
+    // store into the sort area from a later counter read, so read, store, read,
+    // store ... waited out one LDS round trip per index (NB_PLACE_BATCH=0).
+    if (NB_PLACE_BATCH == 2) {  // every key's reads before any store
+        uint32_t st[KPT][KR];
+#pragma unroll
+        for (int p = 0; p < KPT; ++p)
+#pragma unroll
+            for (int j = 0; j < KR; ++j)
+                if (KX ? j < KX : j < (int)k)
+                    st[p][j] = base + (uint64_t)p * NT + tid < n ? lds_at(pk[p][j] >> kHandleShift) : 0u;
+#pragma unroll
+        for (int p = 0; p < KPT; ++p)
+            if (base + (uint64_t)p * NT + tid < n) {
+#pragma unroll
+                for (int j = 0; j < KR; ++j)
+                    if (KX ? j < KX : j < (int)k) lds_at(st[p][j] + (pk[p][j] & kHandleMask)) = ridx[p][j];
+            }
+    } else
 #pragma unroll
     for (int p = 0; p < KPT; ++p) {
         if (base + (uint64_t)p * NT + tid < n) {
+            if (NB_PLACE_BATCH) {
+                uint32_t st[KR];
 #pragma unroll
-            for (int j = 0; j < KR; ++j)
-                if (KX ? j < KX : j < (int)k) {
-                    const uint32_t h = pk[p][j];
-                    lds_at(lds_at(h >> kHandleShift) + (h & kHandleMask)) = ridx[p][j];
-                }
+                for (int j = 0; j < KR; ++j)
+                    if (KX ? j < KX : j < (int)k) st[j] = lds_at(pk[p][j] >> kHandleShift);
+#pragma unroll
+                for (int j = 0; j < KR; ++j)
+                    if (KX ? j < KX : j < (int)k) lds_at(st[j] + (pk[p][j] & kHandleMask)) = ridx[p][j];
+            } else {
+#pragma unroll
+                for (int j = 0; j < KR; ++j)
+                    if (KX ? j < KX : j < (int)k) {
+                        const uint32_t h = pk[p][j];
+                        lds_at(lds_at(h >> kHandleShift) + (h & kHandleMask)) = ridx[p][j];
+                    }
+            }
         }
     }
     const int ovf = ((uint64_t)ga + ua > tc.cap) | ((uint64_t)gb + ub > tc.cap);
