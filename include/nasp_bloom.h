@@ -163,6 +163,13 @@ int nb_builder_add(nb_builder *b, const uint8_t *key, uint64_t len);
  * them has completed); the builds stay asynchronous. */
 int nb_builder_add_batch(nb_builder *b, const uint8_t *keys, const uint64_t *offsets,
                          uint32_t key_len, uint64_t n);
+/* The same, returning once the uploads are enqueued: the caller keeps its buffers
+ * untouched until nb_builder_sync_uploads, nb_builder_finish or nb_builder_destroy
+ * returns (the drop-in class hands it the page-locked chunks it retains anyway, so
+ * packing the next chunk overlaps the DMA of this one). */
+int nb_builder_add_batch_async(nb_builder *b, const uint8_t *keys, const uint64_t *offsets,
+                               uint32_t key_len, uint64_t n);
+int nb_builder_sync_uploads(nb_builder *b);
 /* Build everything added so far and copy the filter to `words` (ceil(m/64) host
  * words).  The builder stays usable: later adds OR into the same filter. */
 int nb_builder_finish(nb_builder *b, uint64_t *words);

@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -295,7 +296,8 @@ __global__ __launch_bounds__(kBlock) void bloom_probe_kernel(
         if (threadIdx.x == 0) {
             uint32_t t = 0;
             for (int w = 0; w < kBlock / 64; ++w) t += wsum[w];
-            gate.hits[blockIdx.x] = t;
+            // system scope: the slot may be host-mapped memory the host spins on
+            __hip_atomic_store(gate.hits + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
 }
@@ -2197,6 +2199,7 @@ TileCfg probe_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
 constexpr uint32_t kProbeSampleBlocks = 16;                 // one key per lane
 constexpr uint64_t kProbeSample = kProbeSampleBlocks * kBlock;  // 4 096 keys
 constexpr uint64_t kProbeTiledMin = 1 << 22;
+constexpr uint32_t kHitsUnset = 0xFFFFFFFFu;  // a sample slot not yet written
 
 template <int FLAVOR, int LAYOUT>
 int launch_probe_lane(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
@@ -2301,6 +2304,8 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     NB_HIP(hipStreamIsCapturing(st, &cs));
     // outside capture the sample's blocks write their counts straight into host-mapped
     // memory (no copy launch); under capture into device words the gated launches read
+    if (cs == hipStreamCaptureStatusNone)  // the previous sample (if any) is complete
+        for (uint32_t b = 0; b < kProbeSampleBlocks; ++b) ws->probe_hits_host[b] = kHitsUnset;
     const ProbeGate sample{cs == hipStreamCaptureStatusNone ? ws->probe_hits_map : ws->probe_hits,
                            nullptr, kProbeSampleBlocks, (uint32_t)S, 1};
     hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, LAYOUT>), dim3(kProbeSampleBlocks), dim3(kBlock), 0,
@@ -2309,10 +2314,24 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     NB_HIP(hipGetLastError());
     if (cs == hipStreamCaptureStatusNone) {
         NB_HIP(hipEventRecord(ws->ev_probe, st));
-        NB_HIP(hipEventSynchronize(ws->ev_probe));
+        // The host polls the slots (reset to a sentinel before the launch; a count is
+        // at most kBlock) instead of sleeping on the event: the chosen path is
+        // launched ~as soon as the sample lands.  Past 20 ms of polling (the stream
+        // busy with long earlier work) it waits on the event instead.
+        volatile uint32_t *hs = ws->probe_hits_host;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spins = 0;; ++spins) {
+            bool all = true;
+            for (uint32_t b = 0; b < kProbeSampleBlocks && all; ++b) all = hs[b] != kHitsUnset;
+            if (all) break;
+            if ((spins & 255) == 255 &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) {
+                NB_HIP(hipEventSynchronize(ws->ev_probe));
+                break;
+            }
+        }
         uint64_t h = 0;
-        for (uint32_t b = 0; b < kProbeSampleBlocks; ++b)
-            h += reinterpret_cast<volatile uint32_t *>(ws->probe_hits_host)[b];
+        for (uint32_t b = 0; b < kProbeSampleBlocks; ++b) h += hs[b];
         if (2 * h >= S) return tiled(rk, ro, n - S, out + S, none);  // as gate_open decides
         return launch_probe_lane<FLAVOR, LAYOUT>(rk, ro, key_len, n - S, c, words, out + S, st, none);
     }

@@ -268,8 +268,28 @@ int nb_builder_add(nb_builder *b, const uint8_t *key, uint64_t len) {
     return NB_OK;
 }
 
+static int add_batch(nb_builder *b, const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
+                     uint64_t n, bool wait_uploads);
+
 int nb_builder_add_batch(nb_builder *b, const uint8_t *keys, const uint64_t *offsets,
                          uint32_t key_len, uint64_t n) {
+    return add_batch(b, keys, offsets, key_len, n, true);
+}
+
+int nb_builder_add_batch_async(nb_builder *b, const uint8_t *keys, const uint64_t *offsets,
+                               uint32_t key_len, uint64_t n) {
+    return add_batch(b, keys, offsets, key_len, n, false);
+}
+
+int nb_builder_sync_uploads(nb_builder *b) {
+    if (!b) return nb_internal_fail(NB_ERR_ARG, "NULL builder");
+    SB_HIP(hipSetDevice(b->ss->dev));
+    SB_HIP(hipStreamSynchronize(b->ss->copy));
+    return NB_OK;
+}
+
+static int add_batch(nb_builder *b, const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
+                     uint64_t n, bool wait_uploads) {
     if (!b) return nb_internal_fail(NB_ERR_ARG, "NULL builder");
     if (n == 0) return NB_OK;
     if (!keys) return nb_internal_fail(NB_ERR_ARG, "NULL keys");
@@ -326,8 +346,9 @@ int nb_builder_add_batch(nb_builder *b, const uint8_t *keys, const uint64_t *off
     }
     b->slot(b->cur).h_offs[0] = 0;
     // every upload from the caller's buffers has landed: they may be reused (the
-    // builds stay in flight)
-    SB_HIP(hipStreamSynchronize(ss->copy));
+    // builds stay in flight).  The async form leaves that to nb_builder_sync_uploads /
+    // finish / destroy.
+    if (wait_uploads) SB_HIP(hipStreamSynchronize(ss->copy));
     return NB_OK;
 }
 
@@ -341,6 +362,7 @@ int nb_builder_finish(nb_builder *b, uint64_t *words) {
         SB_HIP(hipMemcpyAsync(words, b->ss->d_words, b->nwords * 8, hipMemcpyDeviceToHost,
                               b->ss->comp));
     SB_HIP(hipStreamSynchronize(b->ss->comp));
+    SB_HIP(hipStreamSynchronize(b->ss->copy));  // (async batches: their uploads too)
     for (Slot &sl : b->ss->s) sl.busy = false;
     return NB_OK;
 }
@@ -373,6 +395,7 @@ int drain(nb_builder *b) {
     const int rc = b->submit();
     if (rc) return rc;
     SB_HIP(hipStreamSynchronize(b->ss->comp));
+    SB_HIP(hipStreamSynchronize(b->ss->copy));  // (async batches: their uploads too)
     for (Slot &sl : b->ss->s) sl.busy = false;
     return NB_OK;
 }

@@ -266,13 +266,16 @@ void BloomFilter::open_device() const {
     mode = Mode::kHost;
 }
 
+// The chunk's upload is only enqueued: its buffers stay untouched until the builder
+// syncs its uploads (a chunk let go past retainBytes(), finish, destroy).
 bool BloomFilter::stream_chunk(Chunk &c) const {
-    if (c.fixed > 0) return nb_builder_add_batch(stream, c.bytes, nullptr, (uint32_t)c.fixed, c.n) == NB_OK;
+    if (c.fixed > 0)
+        return nb_builder_add_batch_async(stream, c.bytes, nullptr, (uint32_t)c.fixed, c.n) == NB_OK;
     if (c.fixed == 0) {  // all keys empty
         need_offsets(c);
         for (uint64_t i = 0; i <= c.n; ++i) c.offs[i] = 0;
     }
-    return nb_builder_add_batch(stream, c.bytes, c.offs, 0, c.n) == NB_OK;
+    return nb_builder_add_batch_async(stream, c.bytes, c.offs, 0, c.n) == NB_OK;
 }
 
 // The pending batch through nb_build_cpu (the kernels' index arithmetic) into the
@@ -346,7 +349,13 @@ void BloomFilter::hand_off() const {
                     if (retained_all && kept + c.used <= g_retain_bytes) {
                         retained.push_back(c);
                         kept += c.used;
-                    } else {
+                    } else {  // let go: its upload must land before the buffer is reused
+                        if (nb_builder_sync_uploads(stream) != NB_OK) {
+                            retained.push_back(c);  // nothing lost yet: rebuild on the host
+                            moved = true;
+                            device_failed("a chunk upload");
+                            continue;
+                        }
                         retained_all = false;
                         free_chunk(c);
                     }

@@ -75,6 +75,9 @@ _SIGS = {
     "nb_builder_add": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     "nb_builder_add_batch": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
                                        C.c_uint64]),
+    "nb_builder_add_batch_async": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32,
+                                             C.c_uint64]),
+    "nb_builder_sync_uploads": (C.c_int, [C.c_void_p]),
     "nb_builder_finish": (C.c_int, [C.c_void_p, C.c_void_p]),
     "nb_builder_destroy": (C.c_int, [C.c_void_p]),
     "nb_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(C.c_void_p)]),

@@ -225,6 +225,16 @@ class Builder:
         check(lib().nb_builder_add_batch(self._h, _np_ptr(keys), _np_ptr(offsets), key_len, n),
               "nb_builder_add_batch")
 
+    def add_batch_async(self, keys: np.ndarray, offsets: np.ndarray | None, key_len: int,
+                        n: int) -> None:
+        """nb_builder_add_batch_async: the buffers must stay untouched (and alive) until
+        sync_uploads(), finish() or close() returns."""
+        check(lib().nb_builder_add_batch_async(self._h, _np_ptr(keys), _np_ptr(offsets), key_len, n),
+              "nb_builder_add_batch_async")
+
+    def sync_uploads(self) -> None:
+        check(lib().nb_builder_sync_uploads(self._h), "nb_builder_sync_uploads")
+
     def finish(self, words: np.ndarray | None = None) -> np.ndarray:
         if words is None:
             words = np.zeros(max(nwords(self.m), 1), dtype=np.uint64)

@@ -95,6 +95,33 @@ def test_builder_add_batch_c2_full_size(dev, oracle):
     np.testing.assert_array_equal(got[: nbm.nwords(w.m)], want)
 
 
+def test_builder_add_batch_async_buffers_kept(dev, oracle):
+    """nb_builder_add_batch_async: many batches from distinct buffers (fixed and
+    variable-length), enqueued without waiting for their uploads, a sync_uploads in
+    the middle, then finish: bit-exact with the oracle; a second finish after more
+    async batches accumulates."""
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    m, k = synth.C3.m, 7
+    n = 1_200_000
+    parts = [synth.fixed_keys(n, 16, seed=400 + i) for i in range(3)]
+    vb, vo = synth.var_keys(900_000)
+    with nbm.Builder(m, k, SEED) as b:
+        for i, buf in enumerate(parts):
+            b.add_batch_async(buf, None, 16, n)
+            if i == 1:
+                b.sync_uploads()
+        got = b.finish()
+        want = np.zeros(nbm.nwords(m), np.uint64)
+        for buf in parts:
+            want |= oracle.build(0, buf, None, 16, n, m, k, SEED)
+        np.testing.assert_array_equal(got[: nbm.nwords(m)], want)
+        b.add_batch_async(vb, vo, 0, 900_000)
+        got = b.finish()
+    want |= oracle.build(0, vb, vo, 0, 900_000, m, k, SEED)
+    np.testing.assert_array_equal(got[: nbm.nwords(m)], want)
+
+
 @pytest.mark.parametrize("flavor", [0, 1])
 def test_builder_add_batch_varlen_byte_chunks(dev, oracle, flavor):
     """C3's shape (8-64 B keys): chunks cut by bytes, each copied from a 16-byte
