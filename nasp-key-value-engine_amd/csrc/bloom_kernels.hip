@@ -22,7 +22,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -296,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void bloom_probe_kernel(
         if (threadIdx.x == 0) {
             uint32_t t = 0;
             for (int w = 0; w < kBlock / 64; ++w) t += wsum[w];
-            // system scope: the slot may be host-mapped memory the host spins on
+            // system scope: the slot may be host-mapped memory
             __hip_atomic_store(gate.hits + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
@@ -380,6 +379,9 @@ constexpr uint32_t kMaxCurTiles = 8192;  // cursor / spill-flag slots (two-level
 // L2 otherwise merges), non-temporal bucket loads in the tile and re-bin kernels
 // (read once; on by default).  Non-temporal key loads in the bin kernel measured
 // 0.5-1 % slower (C3/C4/C5) and are not used.
+#ifndef NB_WO_UNROLL  // packed write-out: words per lane per step (A/B)
+#define NB_WO_UNROLL 2
+#endif
 #ifndef NB_PLACE_BATCH  // bin placement: a key's run-start reads before its stores (A/B: 0)
 #define NB_PLACE_BATCH 1
 #endif
@@ -690,13 +692,14 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
         if (!any_ovf && b32) {
             char *bb = reinterpret_cast<char *>(buckets);
             uint32_t q = tid;
-            for (; q + NT < words; q += 2 * NT) {
-                uint32_t t[2];
-                uint64_t w[2];
+            constexpr int WU = NB_WO_UNROLL;  // words per lane in flight (their LDS reads overlap)
+            for (; q + (WU - 1) * NT < words; q += WU * NT) {
+                uint32_t t[WU];
+                uint64_t w[WU];
 #pragma unroll
-                for (int u = 0; u < 2; ++u) w[u] = word_at(q + u * NT, &t[u]);
+                for (int u = 0; u < WU; ++u) w[u] = word_at(q + u * NT, &t[u]);
 #pragma unroll
-                for (int u = 0; u < 2; ++u)
+                for (int u = 0; u < WU; ++u)
                     bucket_store(reinterpret_cast<uint64_t *>(bb + (GX[t[u]] + (q + u * NT) * 8u)),
                                  w[u]);
             }
@@ -2199,7 +2202,6 @@ TileCfg probe_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
 constexpr uint32_t kProbeSampleBlocks = 16;                 // one key per lane
 constexpr uint64_t kProbeSample = kProbeSampleBlocks * kBlock;  // 4 096 keys
 constexpr uint64_t kProbeTiledMin = 1 << 22;
-constexpr uint32_t kHitsUnset = 0xFFFFFFFFu;  // a sample slot not yet written
 
 template <int FLAVOR, int LAYOUT>
 int launch_probe_lane(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
@@ -2304,8 +2306,6 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     NB_HIP(hipStreamIsCapturing(st, &cs));
     // outside capture the sample's blocks write their counts straight into host-mapped
     // memory (no copy launch); under capture into device words the gated launches read
-    if (cs == hipStreamCaptureStatusNone)  // the previous sample (if any) is complete
-        for (uint32_t b = 0; b < kProbeSampleBlocks; ++b) ws->probe_hits_host[b] = kHitsUnset;
     const ProbeGate sample{cs == hipStreamCaptureStatusNone ? ws->probe_hits_map : ws->probe_hits,
                            nullptr, kProbeSampleBlocks, (uint32_t)S, 1};
     hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, LAYOUT>), dim3(kProbeSampleBlocks), dim3(kBlock), 0,
@@ -2314,22 +2314,8 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     NB_HIP(hipGetLastError());
     if (cs == hipStreamCaptureStatusNone) {
         NB_HIP(hipEventRecord(ws->ev_probe, st));
-        // The host polls the slots (reset to a sentinel before the launch; a count is
-        // at most kBlock) instead of sleeping on the event: the chosen path is
-        // launched ~as soon as the sample lands.  Past 20 ms of polling (the stream
-        // busy with long earlier work) it waits on the event instead.
+        NB_HIP(hipEventSynchronize(ws->ev_probe));
         volatile uint32_t *hs = ws->probe_hits_host;
-        const auto t0 = std::chrono::steady_clock::now();
-        for (uint32_t spins = 0;; ++spins) {
-            bool all = true;
-            for (uint32_t b = 0; b < kProbeSampleBlocks && all; ++b) all = hs[b] != kHitsUnset;
-            if (all) break;
-            if ((spins & 255) == 255 &&
-                std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) {
-                NB_HIP(hipEventSynchronize(ws->ev_probe));
-                break;
-            }
-        }
         uint64_t h = 0;
         for (uint32_t b = 0; b < kProbeSampleBlocks; ++b) h += hs[b];
         if (2 * h >= S) return tiled(rk, ro, n - S, out + S, none);  // as gate_open decides
