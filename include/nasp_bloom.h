@@ -80,8 +80,12 @@ uint64_t nb_device_merkle_count(void);
  * it for the whole process afterwards (thread-safe).  Names: NB_BUILD_PATH
  * (0 auto, 1 atomic, 2 tiled), NB_PROBE_PATH (0 auto, 1 one lane per key, 2 tiled),
  * NB_PACK, NB_TILE_BITS, NB_SHARDS, NB_CHUNK_KEYS, NB_TWO_LEVEL, NB_PACK5,
- * NB_ENTRY32, NB_RANK, NB_FIXED32, NB_FPMOD, NB_KEXACT, NB_BIN_WIDE, NB_SHARDED_STAGE, NB_FAIL_BUILDS /
- * NB_FAIL_MERKLES (the next N device builds / trees fail with NB_ERR_HIP).
+ * NB_ENTRY32, NB_RANK, NB_FIXED32, NB_FPMOD, NB_KEXACT, NB_BIN_WIDE, NB_OVERLAP (two-level
+ * sub-passes pipelined over a second stream of the workspace: 0 off, 1/2 normal/high
+ * priority, +4 tile kernels beside the next pass's bin kernel; default 6),
+ * NB_SUBPASSES (bin + re-bin sub-passes per tile pass, default 2), NB_FINE_BITS,
+ * NB_SHARDED_STAGE, NB_FAIL_BUILDS / NB_FAIL_MERKLES (the next N device builds /
+ * trees fail with NB_ERR_HIP).
  * Unknown names: NB_ERR_ARG. */
 int nb_set_knob(const char *name, uint64_t value);
 int nb_get_knob(const char *name, uint64_t *value);
@@ -187,7 +191,11 @@ int nb_host_free(void *p);
  * No host synchronisation once the library's per-(device, stream) workspace is
  * large enough; the first call with a larger shape grows it (hipMalloc, stream
  * synchronised), so warm a stream up with its largest shape before capturing it
- * into a hipGraph.  Key memory is read only in aligned 8- and 16-byte granules
+ * into a hipGraph.  Filters of more than 2 048 tiles (m > ~2^31, e.g. 2^32-1) are
+ * built in passes whose re-bin and tile kernels run on a second stream of the
+ * workspace (NB_OVERLAP): it waits on `stream` at entry and `stream` waits on it at
+ * exit (events), so callers -- and stream capture, as a fork/join -- see one
+ * stream.  Key memory is read only in aligned 8- and 16-byte granules
  * that hold key bytes, so a key buffer needs no slack past its last byte and
  * may start at any alignment (16-byte-aligned 16-byte keys take a faster path). */
 int nb_build_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
@@ -209,8 +217,8 @@ int nb_build_device_ex(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_
  * path (lookups binned by filter tile and tested in LDS: ~4x the one-lane-per-key
  * rate for present keys, ~half of it for absent ones); NB_PROBE_PATH=0 (auto)
  * probes the first 4 096 keys one lane per key and picks the tiled path when at
- * least half of them were present.  Auto synchronises `stream` once to read that
- * sample (64 bytes) -- except while the stream is being captured into a graph,
+ * least half of them were present.  Auto waits once for that sample (its 16 counts
+ * land in host-mapped memory) -- except while the stream is being captured into a graph,
  * where both paths are launched and gated on the sample on the device.  Same
  * answers on every path. */
 int nb_probe_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
