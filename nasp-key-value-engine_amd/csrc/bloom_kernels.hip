@@ -343,6 +343,8 @@ constexpr uint32_t kHandleShift = 18, kHandleMask = (1u << kHandleShift) - 1;
 constexpr int kBinThreads = 1024;
 constexpr int kBinThreadsWide = 896;    // 32-byte keys at k = 10: 2 x 896 keys per block
 constexpr int kBinThreads16Wide = 768;  // 16-byte keys at k = 7: 3 x 768 keys per block
+constexpr int kBinThreads3 = 512;       // 16-byte keys at k = 7, few tiles: 2 x 512, 3 blocks/CU
+constexpr uint32_t kThreeBlockTiles = 384;
 constexpr int kBinKPT = 2;       // keys per thread when k <= 8 (1 for larger k)
 constexpr int kTileThreads = 1024;
 constexpr int kTileUnroll = 4;   // 16-byte bucket loads in flight per lane
@@ -2122,9 +2124,21 @@ int launch_build_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         if constexpr (kParity && LAYOUT == kFixed16) {
             // (NB_BIN_WIDE: 768 threads x 3 keys, 2 304 keys per block -- two blocks
             // still fit a CU's LDS at C4's 915 tiles -- at 6 waves per SIMD)
-            if (exact && c.k == 7 && knob(nb::kKnobBinWide) != 0)
+            // Filters of few tiles (C2: 183) run 512 threads x 2 keys, three blocks per
+            // CU: the blocks' runs stay long (~39 entries at T = 183) and three resident
+            // blocks overlap one block's LDS-bound sort with another's VALU-bound hash
+            // (C2 0.137-0.143 -> 0.132-0.136 ms); at C4's 915 tiles the short runs' pads
+            // and reservations cost more (1.68 vs 1.44 ms), so larger filters keep the
+            // 2 304-key blocks.  NB_BIN_WIDE: 1 this policy, 2 / 3 force either.
+            const uint64_t bw = knob(nb::kKnobBinWide);
+            if (exact && c.k == 7 && bw != 0) {
+                const bool three = bw == 2 || (bw == 1 && choose_tiles(c.fm.m, n, c.k).T <= kThreeBlockTiles);
+                if (three)
+                    return launch_tiled<FLAVOR, LAYOUT, 2, kBinThreads3, false, 7, 7>(
+                        keys, offsets, key_len, n, c, words, overwrite, st);
                 return launch_tiled<FLAVOR, LAYOUT, 3, kBinThreads16Wide, false, 7, 7>(
                     keys, offsets, key_len, n, c, words, overwrite, st);
+            }
         }
         if constexpr (kParity && (LAYOUT == kFixed16 || LAYOUT == kOffsets)) {
             if (exact && c.k == 7)

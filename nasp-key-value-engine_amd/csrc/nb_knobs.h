@@ -27,8 +27,11 @@ enum Knob : int {
     kKnobFixed32,       // NB_FIXED32        1: register path for 16-byte-aligned 32-byte keys
     kKnobFpMod,         // NB_FPMOD          1: f64-quotient remainders
     kKnobKExact,        // NB_KEXACT         1: bin kernels specialised for k = 7 / 10
-    kKnobBinWide,       // NB_BIN_WIDE       1: larger bin blocks (2 304 keys for 16-byte keys
-                        //                   at k = 7, 1 792 for 32-byte keys at k = 10)
+    kKnobBinWide,       // NB_BIN_WIDE       1: bin blocks by shape (2 304 keys for 16-byte
+                        //                   keys at k = 7 -- 1 024, three per CU, when the
+                        //                   filter has <= 384 tiles -- 1 792 for 32-byte
+                        //                   keys at k = 10); 2 / 3: force 1 024 / 2 304;
+                        //                   0: the 2 048-key blocks
     kKnobShardedStage,  // NB_SHARDED_STAGE  1: nb_build_sharded stages every merge source
     kKnobOverlap,       // NB_OVERLAP        1: two-level sub-passes pipelined over two
                         //                   streams (sub-pass s's re-bin beside sub-pass
