@@ -344,6 +344,7 @@ constexpr int kBinThreads = 1024;
 constexpr int kBinThreadsWide = 896;    // 32-byte keys at k = 10: 2 x 896 keys per block
 constexpr int kBinThreads16Wide = 768;  // 16-byte keys at k = 7: 3 x 768 keys per block
 constexpr int kBinThreads3 = 512;       // 16-byte keys at k = 7, few tiles: 2 x 512, 3 blocks/CU
+constexpr int kBinThreads3Wide = 576;   // 32-byte keys at k = 10, few tiles: 2 x 576, 3 blocks/CU
 constexpr uint32_t kThreeBlockTiles = 384;
 constexpr int kBinKPT = 2;       // keys per thread when k <= 8 (1 for larger k)
 constexpr int kTileThreads = 1024;
@@ -2149,9 +2150,22 @@ int launch_build_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
             // (NB_BIN_WIDE: 896 threads x 2 keys, 1 792 keys per block -- two blocks of
             // 10 indices per key still fit a CU's LDS -- amortising the per-block scan,
             // reservations and pads over 1.75x the keys)
-            if (exact && c.k == 10 && knob(nb::kKnobBinWide) != 0)
+            // the same shape policy: 576 threads x 2 keys, three blocks per CU, when the
+            // bin kernel's tiles are few -- <= 384 tiles, or the two-level build's 64-128
+            // super tiles (C5 33.64-33.82 -> 33.18-33.43 ms, per-rank share 4.57-4.60 ->
+            // 4.49-4.51 ms); NB_BIN_WIDE 4 / 3 force either
+            const uint64_t bw = knob(nb::kKnobBinWide);
+            if (exact && c.k == 10 && bw != 0) {
+                const uint32_t T = choose_tiles(c.fm.m, n, c.k).T;
+                const bool three = bw == 4 || (bw == 1 && (T <= kThreeBlockTiles ||
+                                                           (T > 2u * kBinThreadsWide &&
+                                                            knob(nb::kKnobTwoLevel) != 0)));
+                if (three)
+                    return launch_tiled<FLAVOR, LAYOUT, 2, kBinThreads3Wide, false, 10, 10>(
+                        keys, offsets, key_len, n, c, words, overwrite, st);
                 return launch_tiled<FLAVOR, LAYOUT, 2, kBinThreadsWide, false, 10, 10>(
                     keys, offsets, key_len, n, c, words, overwrite, st);
+            }
             if (exact && c.k == 10)
                 return launch_tiled<FLAVOR, LAYOUT, 1, kBinThreads, false, 10, 10>(
                     keys, offsets, key_len, n, c, words, overwrite, st);

@@ -29,9 +29,11 @@ enum Knob : int {
     kKnobKExact,        // NB_KEXACT         1: bin kernels specialised for k = 7 / 10
     kKnobBinWide,       // NB_BIN_WIDE       1: bin blocks by shape (2 304 keys for 16-byte
                         //                   keys at k = 7 -- 1 024, three per CU, when the
-                        //                   filter has <= 384 tiles -- 1 792 for 32-byte
-                        //                   keys at k = 10); 2 / 3: force 1 024 / 2 304;
-                        //                   0: the 2 048-key blocks
+                        //                   filter has <= 384 tiles -- and 1 792 for
+                        //                   32-byte keys at k = 10 -- 1 152, three per CU,
+                        //                   for <= 384 tiles or two-level pass 1); 2 / 3:
+                        //                   force 1 024 / 2 304, 4: force 1 152; 0: the
+                        //                   2 048-key (1 024 for k = 10) blocks
     kKnobShardedStage,  // NB_SHARDED_STAGE  1: nb_build_sharded stages every merge source
     kKnobOverlap,       // NB_OVERLAP        1: two-level sub-passes pipelined over two
                         //                   streams (sub-pass s's re-bin beside sub-pass

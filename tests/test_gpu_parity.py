@@ -787,12 +787,13 @@ def test_cooperative_build_single_rank(dev, oracle):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kexact,wide", [(0, 0), (1, 0), (1, 1), (1, 2), (1, 3)])
+@pytest.mark.parametrize("kexact,wide", [(0, 0), (1, 0), (1, 1), (1, 2), (1, 3), (1, 4)])
 def test_exact_k_kernels(dev, oracle, knobs, kexact, wide):
     """The bin kernels specialised for k = 7 (16-byte and variable-length keys;
     NB_BIN_WIDE=1: 2 304-key blocks, or 1 024-key blocks three per CU for filters
     of <= 384 tiles, 2 / 3 forcing either) and k = 10 (32-byte keys; NB_BIN_WIDE:
-    1 792-key blocks), and the general
+    1 792-key blocks, or 1 152-key blocks three per CU for few tiles and two-level
+    pass 1, 4 forcing them), and the general
     k <= 8 / k <= 16 kernels they replace (NB_KEXACT=0), give the same bits as the
     oracle -- both flavours, chunked, single- and two-level."""
     from nasp_bloom import synth
