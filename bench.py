@@ -529,14 +529,18 @@ def bench_cooperative(args, wl, world, rank, dev):
     seed = synth.H2_SEED
     stream = torch.cuda.current_stream(dev)
 
+    # the gloo rehearsal (NB_BENCH_BACKEND) exchanges the slices through host copies
+    comm = None if os.environ.get("NB_BENCH_BACKEND", "nccl") == "nccl" else "cpu"
+
     def step(host_out=None):
         # each rank ends with its owned word slice (no all-gather of the whole filter
         # to every rank: the filter is written out slice by slice)
         return D.build_cooperative(keys, None, wl.key_len, n, wl.m, wl.k, seed, args.flavor,
-                                   all_gather=False, host_out=host_out)
+                                   all_gather=False, host_out=host_out, comm_device=comm)
 
     # correctness guard (untimed): the all-gathered filter has no false negative
-    full = D.build_cooperative(keys, None, wl.key_len, n, wl.m, wl.k, seed, args.flavor)
+    full = D.build_cooperative(keys, None, wl.key_len, n, wl.m, wl.k, seed, args.flavor,
+                               comm_device=comm)
     torch.cuda.synchronize(dev)
     out = torch.empty(n, dtype=torch.uint8, device=dev)
     nbm.probe_device(keys, None, wl.key_len, n, wl.m, wl.k, seed, args.flavor, full, out)
