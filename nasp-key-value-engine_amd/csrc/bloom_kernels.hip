@@ -224,7 +224,7 @@ using nb::IndexGen;
 
 // Path A ("atomic"): one lane per key, k no-return agent-scope atomic ORs.
 // Bounded by the chip's atomic request rate (~27 G/s measured, tools/ubench.hip),
-// used for k > 16, for filters too large for the tiled path, and for tiny batches.
+// used for k > 32, for filters too large for the tiled path, and for tiny batches.
 template <int FLAVOR, int LAYOUT>
 __global__ __launch_bounds__(kBlock) void bloom_build_atomic_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
@@ -2225,6 +2225,17 @@ TileCfg probe_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     return tc;
 }
 
+// LDS of the tiled probe's bin kernel: counters, scan and run tables, then the
+// block's indices sorted by tile and their keys (or the staged key bytes).  Must fit
+// one workgroup's 160 KiB: 32-byte keys at k = 12..16 over 4 096 tiles do not
+// (163 968 B at k = 12), and those batches take the lane path.
+constexpr size_t kMaxBlockLds = 160 * 1024;
+size_t probe_bin_lds_bytes(uint32_t T, uint32_t k, bool stage) {
+    size_t sort_bytes = (size_t)2 * kProbeThreads * k * 4;
+    if (stage) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(kProbeThreads));
+    return (size_t)probe_sort_offset_words(T) * 4 + sort_bytes;
+}
+
 // Auto mode's sample (the first kProbeSample keys, probed by the lane kernel) and
 // the smallest batch the tiled path is considered for.
 constexpr uint32_t kProbeSampleBlocks = 16;                 // one key per lane
@@ -2259,9 +2270,8 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
     const uint64_t chunk = std::max<uint64_t>(1, (n + passes - 1) / passes);
     const TileCfg tc = probe_tiles(c.fm.m, chunk, c.k);
     if ((rc = ws_reserve(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * 8, &sc))) return rc;
-    size_t sort_bytes = (size_t)2 * NT * c.k * 4;
-    if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(NT));
-    const size_t bin_lds = (size_t)probe_sort_offset_words(tc.T) * 4 + sort_bytes;
+    const size_t bin_lds = probe_bin_lds_bytes(tc.T, c.k, STAGE);
+    if (bin_lds > kMaxBlockLds) return fail(NB_ERR_UNSUPPORTED, "tiled probe: LDS of the shape");
     const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
     auto bin = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR>;
     auto tile = probe_tile_kernel<kTileThreads>;
@@ -2292,8 +2302,9 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     const uint64_t path = knob(nb::kKnobProbePath);
     constexpr bool kTiledLayout = LAYOUT != kFixedStride && FLAVOR != NB_FLAVOR_MURMUR3_X64_128;
     const uint32_t kmax = LAYOUT == kFixed32 ? 16u : 8u;
-    const bool tiled_ok = kTiledLayout && c.k <= kmax &&
-                          probe_tiles(c.fm.m, n, c.k).T <= kMaxTiles;
+    const uint32_t pT = probe_tiles(c.fm.m, n, c.k).T;
+    const bool tiled_ok = kTiledLayout && c.k <= kmax && pT <= kMaxTiles &&
+                          probe_bin_lds_bytes(pT, c.k, !vec_layout(LAYOUT)) <= kMaxBlockLds;
     const ProbeGate none{nullptr, nullptr, 0, 0, 0};
     if (path == 1 || !tiled_ok || (path == 0 && n < kProbeTiledMin))
         return launch_probe_lane<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, out, st, none);

@@ -35,11 +35,14 @@ enum Knob : int {
                         //                   force 1 024 / 2 304, 4: force 1 152; 0: the
                         //                   2 048-key (1 024 for k = 10) blocks
     kKnobShardedStage,  // NB_SHARDED_STAGE  1: nb_build_sharded stages every merge source
-    kKnobOverlap,       // NB_OVERLAP        1: two-level sub-passes pipelined over two
-                        //                   streams (sub-pass s's re-bin beside sub-pass
-                        //                   s+1's bin kernel); 2: the same, the second
-                        //                   stream at high priority
-    kKnobSubpasses,     // NB_SUBPASSES      bin + re-bin sub-passes per tile pass (1)
+    kKnobOverlap,       // NB_OVERLAP        bit field (default 6): & 3 == 1: two-level
+                        //                   sub-passes pipelined over two streams (sub-pass
+                        //                   s's re-bin beside sub-pass s+1's bin kernel),
+                        //                   & 3 == 2: the same, the second stream at high
+                        //                   priority; + 4: a pass's first bin kernel does
+                        //                   not wait for the previous pass's tile kernel;
+                        //                   0: no pipelining
+    kKnobSubpasses,     // NB_SUBPASSES      bin + re-bin sub-passes per tile pass (2)
     kKnobFineBits,      // NB_FINE_BITS      0: fine-tile policy (2^20 bits); 19: 2^19-bit fine
                         //                   tiles in the two-level build
     kKnobProbePath,     // NB_PROBE_PATH     0 auto | 1 "lane" (one lane per key) | 2 "tiled"

@@ -96,7 +96,9 @@ def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len:
     `host_out` (a host tensor of >= S int64 words, pinned for an asynchronous copy)
     that slice is downloaded into it -- the filter then ends in host memory, each
     owner holding its part of SSTable::build's filter block (SURVEY §5: per-slice
-    D2H instead of an all-gather)."""
+    D2H instead of an all-gather).  The call returns once that download has landed
+    (an event recorded behind the copy is waited for), so the caller may write the
+    returned host slice to disk at once."""
     world = dist.get_world_size(group)
     S = slice_words(m, world)
     if build_fn is None:
@@ -117,6 +119,12 @@ def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len:
         if host_out.numel() < out.numel():
             raise ValueError("host_out holds fewer words than the owned slice")
         host_out[: out.numel()].copy_(out, non_blocking=host_out.is_pinned())
+        if host_out.is_pinned() and out.is_cuda:
+            # the copy is asynchronous: wait for it before the host words are handed
+            # back
+            landed = torch.cuda.Event()
+            landed.record(torch.cuda.current_stream(out.device))
+            landed.synchronize()
         return host_out[: out.numel()]
     return out
 

@@ -307,3 +307,27 @@ def test_engine_small_flush_stays_on_host(tmp_path, built):
         same_files(d_ref, d_new)
         assert device_counts(err) == want, err
         assert "GPU build failed" not in err
+
+
+@pytest.mark.gpu
+def test_engine_flush_survives_injected_device_failure(tmp_path, built):
+    """A device failure in the middle of an engine flush (NB_FAIL_BUILDS=1: the first
+    device filter build returns NB_ERR_HIP) is reported once on stderr and the filter
+    is rebuilt on the host from the keys the class retains (6 000 keys, far below
+    BloomFilter::retainBytes()), so SSTManager::write completes and every file is
+    still the reference engine's, byte for byte (the throw past the
+    retention budget is the only way the class reports a device fault, and an engine
+    that must never see it sets BloomFilter::setRetainBytes(UINT64_MAX) --
+    INTEGRATION.md section 1)."""
+    if not (os.path.exists(DROPIN_ENGINE) and os.path.exists(REF_ENGINE)):
+        pytest.skip("engine binaries not built (need /root/reference at build time)")
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    n, bs, t = 6000, 4096, 1748963255
+    d_ref, d_new = tmp_path / "ref", tmp_path / "dropin"
+    run_engine(REF_ENGINE, d_ref, "raw", n, bs, fixed_time=t)
+    _, err = run_engine(DROPIN_ENGINE, d_new, "raw", n, bs, fixed_time=t,
+                        extra_env={"NB_FAIL_BUILDS": "1"}, want_stderr=True)
+    same_files(d_ref, d_new)
+    assert err.count("[BloomFilter] GPU build failed (injected device build failure") == 1

@@ -119,3 +119,23 @@ def test_tiled_probe_c4_full_size(dev, knobs):
     assert torch.equal(outs["tiled"], outs["lane"])
     fp = float(outs["lane"][w.n:].float().mean())
     assert 0.008 < fp < 0.012
+
+
+@pytest.mark.parametrize("path", ["tiled", "auto"])
+@pytest.mark.parametrize("k", [11, 12, 16])
+def test_probe_32byte_keys_large_k_full_filter(dev, oracle, knobs, path, k):
+    """32-byte keys at k = 11..16 over m = 2^32 - 1 (4 096 probe tiles): the tiled bin
+    kernel's LDS (sorted indices + their keys) fits a workgroup's 160 KiB up to k = 11
+    and not from k = 12 on (163 968 B), so those batches must take the lane path --
+    before the auto sample writes anything -- and still answer bit-exactly (ADVICE
+    r03: the tiled launch used to fail with NB_ERR_HIP)."""
+    from nasp_bloom import synth
+    knobs(NB_PROBE_PATH=path)
+    n, m = 4_200_000, 2**32 - 1
+    buf = synth.fixed_keys(n, 32, seed=11)
+    npres = int(n * 0.6)
+    words = device_words(dev, buf, None, 32, npres, m, k)
+    got = dev_probe(dev, buf, None, 32, n, m, k, SEED, words)
+    want = oracle.probe(0, buf, None, 32, n, m, k, SEED, words)
+    np.testing.assert_array_equal(got, want)
+    assert got[:npres].all()

@@ -15,6 +15,7 @@ CSRC = os.path.join(REPO, "nasp-key-value-engine_amd", "csrc")
 def main():
     want = sys.argv[1] if len(sys.argv) > 1 else "bloom_bin_kernelILi0ELi2ELi2EtLi1024ELb0ELi8E"
     s = open(os.path.join(CSRC, "bloom_kernels.hip")).read()
+    s = s.replace('#include "nb_knobs.h"', f'#include "{CSRC}/nb_knobs.h"')
     s = s.replace('#include "bloom_math.h"', f'#include "{CSRC}/bloom_math.h"')
     s = s.replace('#include "../../include/nasp_bloom.h"', f'#include "{REPO}/include/nasp_bloom.h"')
     s = s.replace("    if (NB_DIAG_STOP(1)) return;", '    asm volatile(";NBMARK phase2");\n    if (NB_DIAG_STOP(1)) return;')
