@@ -274,6 +274,24 @@ def valu_frac_of(sq):
     return round(sum(v["valu_floor_us"] for v in ks) / sum(v["avg_duration_us"] for v in ks), 4)
 
 
+def rank_diag(per_rank, key):
+    """N > 1 self-diagnosis: the world size and the backend the
+    process group reports, each rank's own numbers, and the min / max of `key`."""
+    import torch.distributed as dist
+    import torch
+    vals = [r[key] for r in per_rank]
+    backend = str(dist.get_backend())
+    nccl = None
+    if backend == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            nccl = ".".join(map(str, v)) if isinstance(v, tuple) else str(v)
+        except Exception:  # noqa: BLE001
+            nccl = "unknown"
+    return {"world_size": dist.get_world_size(), "backend": backend, "rccl_version": nccl,
+            f"{key}_min": min(vals), f"{key}_max": max(vals), "per_rank": per_rank}
+
+
 def reduce_device(dev):
     """Where the max-over-ranks timing tensor lives: the GPU for RCCL, the host for
     the gloo rehearsal (NB_BENCH_BACKEND)."""
@@ -381,10 +399,15 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
 
+    ranks = None
     if world > 1:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=reduce_device(dev))
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        per = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(per, t)
+        ranks = rank_diag([{"elapsed_s": round(float(x[0]), 5), "kern_ms": round(float(x[1]), 5)}
+                           for x in per], "kern_ms")
+        elapsed = max(float(x[0]) for x in per)
+        kern_ms = max(float(x[1]) for x in per)
 
     total_keys = wl.n * args.steps * world
     value = total_keys / elapsed / 1e6
@@ -412,6 +435,8 @@ def main():
                       "flavor": ["libstdc++", "msvc-fnv1a"][args.flavor],
                       "parallelism": f"independent filter per GPU x{world}"},
            "roofline": roofline}
+    if ranks is not None:
+        out["ranks"] = ranks
     if rank == 0 and world == 1 and args.workload == "c4" and not args.no_c2:
         out["c2"] = c2_rate(nbm, synth, dev, stream, args.flavor)
     if rank == 0 and world == 1 and not args.no_probe:
@@ -588,7 +613,28 @@ def bench_cooperative(args, wl, world, rank, dev):
                                    "pinned host memory (the filter ends in host memory)"},
            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                        "kernel": "whole cooperative step per GPU (build + merge collectives)"}}
+                        "kernel": "whole cooperative step per GPU (build + merge collectives)",
+                        "algorithmic_bytes_per_launch": B}}
+    if world == 1:
+        # the one-rank step is the build alone: its measured HBM bytes per step (every
+        # bin / re-bin / tile pass) from the committed PMC summary of these kernels
+        pmc = latest_profile(wl.name, "pmc")
+        res["roofline"]["traffic"] = (pmc or {}).get("hbm_bytes_per_launch")
+        res["roofline"]["traffic_source"] = (pmc or {}).get("source")
+    if world > 1:
+        # one instrumented step (untimed above): per rank, the build, all-to-all, OR
+        # kernel and D2H of its owned slice, from events on the step's stream
+        marks = []
+        D.build_cooperative(keys, None, wl.key_len, n, wl.m, wl.k, seed, args.flavor,
+                            all_gather=False, host_out=host, comm_device=comm, marks=marks)
+        mine = D.phase_ms(marks)
+        names = ("build", "all_to_all", "or_merge", "d2h")
+        t = torch.tensor([mine.get(x, -1.0) for x in names], dtype=torch.float64, device=reduce_device(dev))
+        per = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(per, t)
+        res["ranks"] = rank_diag([{x: round(float(v), 4) for x, v in zip(names, p)} for p in per],
+                                 "build")
+        res["ranks"]["comm_device"] = comm or "gpu (RCCL over xGMI)"
     if world == 1 and not args.no_rank_share:
         res["per_rank_at_8"] = rank_share_rate(nbm, wl, keys, seed, args.flavor, dev, stream)
     if rank == 0:

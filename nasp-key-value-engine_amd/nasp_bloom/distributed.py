@@ -49,9 +49,28 @@ def _hip_merge(dst: torch.Tensor, recv: torch.Tensor, nsrc: int, stride: int) ->
     or_merge_device(dst, recv, dst.numel(), nsrc, stride)
 
 
+def _mark(marks: list | None, name: str, device) -> None:
+    """Phase boundary of an instrumented step (bench.py's N > 1 diagnostics): a timing
+    event recorded on the current stream of `device`, appended as (name, event)."""
+    if marks is not None and torch.device(device).type == "cuda":
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(device))
+        marks.append((name, ev))
+
+
+def phase_ms(marks: list) -> dict:
+    """Milliseconds between consecutive marks, keyed by the later mark's name
+    (synchronises on the last event)."""
+    if not marks:
+        return {}
+    marks[-1][1].synchronize()
+    return {name: round(prev.elapsed_time(ev), 4)
+            for (_, prev), (name, ev) in zip(marks[:-1], marks[1:])}
+
+
 def merge_partials(partial: torch.Tensor, m: int, group=None, all_gather: bool = True,
                    merge_fn: Callable | None = None, exchange_single: bool = False,
-                   comm_device=None) -> torch.Tensor:
+                   comm_device=None, marks: list | None = None) -> torch.Tensor:
     """OR-merge every rank's full-size partial filter (int64 tensor of >= world*S
     words, padding zero).  Returns the whole merged filter (all_gather=True) or this
     rank's owned slice of S words (words [rank*S, (rank+1)*S) of the filter).  With
@@ -60,7 +79,9 @@ def merge_partials(partial: torch.Tensor, m: int, group=None, all_gather: bool =
     tests of the RCCL path on a one-GPU box).  comm_device: where the exchanged
     slices live for the collectives (default: the partial's device, i.e. RCCL over
     xGMI); "cpu" routes them through host copies, so a gloo group -- e.g. ranks that
-    share one GPU -- runs the same sequence with the HIP build and OR kernels."""
+    share one GPU -- runs the same sequence with the HIP build and OR kernels.
+    marks: a list that receives a timing event after each phase ("all_to_all",
+    "or_merge", "all_gather"), see phase_ms."""
     world = dist.get_world_size(group)
     S = slice_words(m, world)
     if partial.numel() < world * S:
@@ -73,14 +94,18 @@ def merge_partials(partial: torch.Tensor, m: int, group=None, all_gather: bool =
     recv_c = torch.empty_like(send_c)
     dist.all_to_all_single(recv_c, send_c, group=group)     # recv[j*S:(j+1)*S] = slice of rank j
     recv = recv_c if cd == partial.device else recv_c.to(partial.device)
+    _mark(marks, "all_to_all", partial.device)
     owned = torch.zeros(S, dtype=partial.dtype, device=partial.device)
     (merge_fn or _hip_merge)(owned, recv, world, S)
+    _mark(marks, "or_merge", partial.device)
     if not all_gather:
         return owned
     owned_c = owned if cd == partial.device else owned.to(cd)
     full_c = torch.empty(world * S, dtype=partial.dtype, device=cd)
     dist.all_gather_into_tensor(full_c, owned_c, group=group)
-    return full_c if cd == partial.device else full_c.to(partial.device)
+    full = full_c if cd == partial.device else full_c.to(partial.device)
+    _mark(marks, "all_gather", partial.device)
+    return full
 
 
 def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len: int, n: int,
@@ -88,7 +113,8 @@ def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len:
                       all_gather: bool = True, build_fn: Callable | None = None,
                       merge_fn: Callable | None = None, stream=None,
                       exchange_single: bool = False, comm_device=None,
-                      host_out: torch.Tensor | None = None) -> torch.Tensor:
+                      host_out: torch.Tensor | None = None,
+                      marks: list | None = None) -> torch.Tensor:
     """Cooperative single-filter build.  `keys`/`offsets` hold THIS rank's key range
     (offsets relative to `keys`, n+1 entries; or fixed key_len).  Every rank passes
     the same (m, k, seed, flavor).  all_gather=False leaves each rank with its owned
@@ -98,7 +124,8 @@ def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len:
     owner holding its part of SSTable::build's filter block (SURVEY §5: per-slice
     D2H instead of an all-gather).  The call returns once that download has landed
     (an event recorded behind the copy is waited for), so the caller may write the
-    returned host slice to disk at once."""
+    returned host slice to disk at once.  marks: timing events after each phase
+    ("build", then merge_partials' phases, then "d2h"), see phase_ms."""
     world = dist.get_world_size(group)
     S = slice_words(m, world)
     if build_fn is None:
@@ -107,14 +134,16 @@ def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len:
         partial[nwords(m):].zero_()
     else:  # a test-side builder may OR into the words
         partial = torch.zeros(world * S, dtype=torch.int64, device=keys.device)
+    _mark(marks, "start", keys.device)
     if build_fn is None:
         build_device(keys, offsets, key_len, n, m, k, seed, flavor, partial, stream=stream,
                      overwrite=True)
     else:
         build_fn(keys, offsets, key_len, n, m, k, seed, flavor, partial)
+    _mark(marks, "build", keys.device)
     out = merge_partials(partial, m, group=group, all_gather=all_gather and host_out is None,
                          merge_fn=merge_fn, exchange_single=exchange_single,
-                         comm_device=comm_device)
+                         comm_device=comm_device, marks=marks)
     if host_out is not None:
         if host_out.numel() < out.numel():
             raise ValueError("host_out holds fewer words than the owned slice")
@@ -125,6 +154,7 @@ def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len:
             landed = torch.cuda.Event()
             landed.record(torch.cuda.current_stream(out.device))
             landed.synchronize()
+        _mark(marks, "d2h", out.device)
         return host_out[: out.numel()]
     return out
 

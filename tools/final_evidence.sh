@@ -7,7 +7,7 @@
 set -u
 TAG=${1:-r02e}
 for w in c4 c2 c3 c5; do bash tools/profile_round.sh "$TAG" "$w" || exit 1; done
-for w in c4 c2 c3; do python3 tools/pmc_traffic.py "$TAG" "$w" "gpurun_out/prof_${TAG}_$w" || exit 2; done
+for w in c4 c2 c3 c5; do python3 tools/pmc_traffic.py "$TAG" "$w" "gpurun_out/prof_${TAG}_$w" || exit 2; done
 for w in c4 c2 c3 c5; do
   python3 tools/sq_summary.py "$TAG" "$w" "gpurun_out/prof_${TAG}_$w/sq/run_counter_collection.csv" || exit 3
 done

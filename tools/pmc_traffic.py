@@ -49,17 +49,24 @@ def main(tag, wl_key, prof_dir):
     write = per_kernel(os.path.join(prof_dir, "write", "run_counter_collection.csv"), "WRITE_SIZE")
     parts = {}
     for name in fetch:
-        if "bloom_bin_kernel" in name or "bloom_tile_or_kernel" in name:
+        if any(x in name for x in ("bloom_bin_kernel", "bloom_tile_or_kernel", "bloom_rebin_kernel")):
             f, w = fetch[name], write.get(name, 0.0)
             parts[short(name)] = {"FETCH_SIZE_KB": round(f, 1), "WRITE_SIZE_KB": round(w, 1),
                                   "hbm_bytes": int((2 * f + w) * 1024)}
-    # one bench build = the bin kernel + the overwrite-mode tile kernel
-    # (OR-mode tile calls in the profile come from bench's host-path leg)
-    used = [k for k in parts if "bloom_bin_kernel" in k or ("tile_or" in k and "true" in k)]
-    total = sum(parts[k]["hbm_bytes"] for k in used)
     stats = {}
     for r in csv.DictReader(open(os.path.join(prof_dir, "trace", "run_kernel_stats.csv"))):
         stats[short(r["Name"])] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
+    # one bench step = one build call: exactly one overwrite-mode tile kernel (the
+    # first tile pass), plus per step the same number of bin / re-bin / OR-mode tile
+    # launches (C4: bin + tile; C5: 16 bin + 16 re-bin + 1 overwrite + 7 OR-mode tile
+    # passes).  Per-step bytes = sum over those kernels of the per-dispatch average x
+    # dispatches / steps (the profiled runs skip bench's host-path and probe legs)
+    used = [k for k in parts if k in stats]
+    ow = [k for k in used if "tile_or" in k and "true" in k]
+    steps = sum(stats[k]["calls"] for k in ow) or 1
+    total = sum(parts[k]["hbm_bytes"] * stats[k]["calls"] / steps for k in used)
+    for k in used:
+        parts[k]["dispatches_per_step"] = round(stats[k]["calls"] / steps, 3)
     out = {"workload": wl.name, "kernel_source_sha": kernel_sha(),
            "hbm_bytes_per_launch": int(total), "build_kernels": used, "per_kernel": parts,
            "kernel_stats": stats,
