@@ -316,15 +316,32 @@ __global__ __launch_bounds__(kBlock) void bloom_probe_kernel(
 // (pathological inputs only, e.g. massively duplicated keys) spills the extra
 // indices into a zero-kept spill bitmap that the tile kernel folds in and clears,
 // so results never depend on capacity.
+//
+// The tile of index r is __umulhi(r, mul).  Power-of-two tiles: mul = 2^(32 - ts),
+// i.e. r >> ts.  Counted tiles (round 4, the single-level packed path): any T, with
+// mul = floor(2^32 T / m); tile t is then the bits [start(t), start(t + 1)),
+// start(t) = ceil(t 2^32 / mul), all within a bit of m / T long -- so T can be a
+// whole number of tile-kernel rounds on the chip's 256 CUs (C4: 768 tiles of ~1.25M
+// bits, three rounds, instead of 915 of 2^20 bits, 3.57 rounds).  Tile boundaries
+// then fall inside filter words: the tile kernel ORs its two boundary words in with
+// 64-bit atomics (the bin kernel zeroes them first when the build overwrites).
 struct TileCfg {
-    uint32_t ts;     // log2 bits per tile
-    uint32_t T;      // number of tiles = ceil(m / 2^ts)
+    uint32_t ts;     // log2 bits per tile (counted tiles: the in-tile offset bits, 21)
+    uint32_t T;      // number of tiles
     uint32_t G;      // cursor/bucket shards per tile
     uint32_t cap;    // capacity (entries) of one (tile, shard) bucket, multiple of 8
     uint32_t fts;    // log2 bits of the tiles the spill flags index: ts, except in
                      // pass 1 of the two-level build (super tiles), where it is the
                      // fine tiles' ts
+    uint32_t mul;    // tile of r = __umulhi(r, mul)
+    uint32_t fmul;   // spill-flag tile of r = __umulhi(r, fmul) (the fts tiling)
+    uint32_t w64;    // LDS words (u64) of one tile in the tile kernel, boundary words incl.
 };
+
+__host__ __device__ inline uint64_t tile_start(uint32_t t, uint32_t mul) {
+    return (((uint64_t)t << 32) + mul - 1) / mul;
+}
+__host__ __device__ inline uint32_t pow2_mul(uint32_t ts) { return 1u << (32 - ts); }
 
 // Bucket unit of pass 1 of the two-level build: five 25-bit in-super-tile offsets
 // per 16 bytes (3.2 B per entry instead of a 32-bit index).
@@ -492,6 +509,8 @@ struct TileScratch {
     uint32_t *gcur;       // [G][T] bucket cursors (zero between builds)
     uint32_t *spill_flag; // [T]    (zero between builds)
     uint32_t *spill32;    // [2*ceil(m/64)] spill bitmap (zero between builds)
+    uint64_t *zero_words = nullptr;  // counted tiles, overwrite: the filter, whose words
+                                     // holding a tile boundary the bin kernel zeroes
 };
 
 // Phases 2-4 of the bin kernel in rank mode when T <= 2 NT: thread tid owns the
@@ -672,7 +691,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
                     const uint32_t v = s5[r];
                     __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31),
                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    sc.spill_flag[v >> tc.fts] = 1u;
+                    sc.spill_flag[__umulhi(v, tc.fmul)] = 1u;
                 }
             }
         }
@@ -685,7 +704,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
         // b[11,ts) | c << 10 -- 5 VALU instead of the 64-bit shifts' 7-8 (17 <= ts <= 20)
         auto word_at = [&](uint32_t q, uint32_t *t) {
             const uint32_t a = sorted[3 * q], b = sorted[3 * q + 1], c = sorted[3 * q + 2];
-            *t = a >> tc.ts;
+            *t = __umulhi(a, tc.mul);
             if (!NB_PACK_HALVES)
                 return (uint64_t)(a & msk) | ((uint64_t)(b & msk) << 21) | ((uint64_t)(c & msk) << 42);
             const uint32_t lo = (a & msk) | (b << 21);
@@ -723,7 +742,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
                         const uint32_t v = sorted[3 * q + r];
                         __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31),
                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        sc.spill_flag[v >> tc.fts] = 1u;
+                        sc.spill_flag[__umulhi(v, tc.fmul)] = 1u;
                     }
                 }
             }
@@ -776,7 +795,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
                 } else {
                     __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
-                    sc.spill_flag[v >> tc.fts] = 1u;
+                    sc.spill_flag[__umulhi(v, tc.fmul)] = 1u;
                 }
             }
         }
@@ -802,7 +821,7 @@ struct BinPhase1 {
 
     __device__ __forceinline__ void run(const uint8_t *__restrict__ keys,
                                         const uint64_t *__restrict__ offsets, uint32_t key_len,
-                                        uint64_t n, const FilterConsts &c, uint32_t ts, uint32_t T,
+                                        uint64_t n, const FilterConsts &c, uint32_t tmul, uint32_t T,
                                         uint32_t *cnt, uint32_t *sorted, uint32_t *any_flag,
                                         uint64_t base) {
         const uint32_t tid = threadIdx.x;
@@ -828,13 +847,13 @@ struct BinPhase1 {
                     if (KX ? j < KX : j < (int)c.k) {
                         if (j) g.next(c);
                         ridx[p][j] = g.r;
-                        rank[p][j] = NB_DIAG_NOCOUNT ? g.r : atomicAdd(&cnt[g.r >> ts], 4u);
+                        rank[p][j] = NB_DIAG_NOCOUNT ? g.r : atomicAdd(&cnt[__umulhi(g.r, tmul)], 4u);
                     }
                 }
             } else {
                 for (uint32_t j = 0; j < c.k; ++j) {
                     if (j) g.next(c);
-                    atomicAdd(&cnt[g.r >> ts], 1u);
+                    atomicAdd(&cnt[__umulhi(g.r, tmul)], 1u);
                 }
             }
         };
@@ -993,6 +1012,11 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     uint32_t *sorted = lds + bin_sort_offset_words(T);  // [KPB * k], 16-byte aligned
     const uint32_t tid = threadIdx.x;
     NB_DIAG_PROLOGUE();
+    if (sc.zero_words && tid == 0)  // counted tiles, overwrite: see TileCfg
+        for (uint32_t t = blockIdx.x + 1; t < T; t += gridDim.x) {
+            const uint64_t b = tile_start(t, tc.mul);
+            if (b & 63) sc.zero_words[b >> 6] = 0;
+        }
     // rank mode (KR > 0): cnt[t] starts at A_t << 18, A_t = the LDS byte address of
     // cnt[t] (< 2^14: the counters lead the LDS, T <= 4 096), and each index adds 4,
     // so the count atomic returns its index's placement handle pk = A_t << 18 |
@@ -1005,7 +1029,7 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     const uint64_t base = (uint64_t)blockIdx.x * (KPT * NT);
     constexpr int kR = KR > 0 ? KR : 1;
     BinPhase1<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, KX> ph;
-    ph.run(keys, offsets, key_len, n, c, tc.ts, T, cnt, sorted, wave_sums + NT / 64 + 1, base);
+    ph.run(keys, offsets, key_len, n, c, tc.mul, T, cnt, sorted, wave_sums + NT / 64 + 1, base);
     IndexGen (&gen)[KPT] = ph.gen;
     const uint32_t (&ridx)[KPT][kR] = ph.ridx;
     const uint32_t (&rank)[KPT][kR] = ph.rank;
@@ -1333,14 +1357,20 @@ template <typename ENTRY, bool OVERWRITE, int NT = kTileThreads, int UNROLL = kT
 __global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
     TileCfg tc, TileScratch sc, const ENTRY *__restrict__ buckets, uint64_t *__restrict__ words,
     uint64_t nwords) {
-    extern __shared__ uint32_t tile[];  // [2^ts / 32] tile words, then 2*kShards+1 words
+    extern __shared__ uint32_t tile[];  // [2 w64] tile words, then 2*kShards+1 words
     constexpr uint32_t kPerVec = 16 / sizeof(ENTRY);  // entries per 16-byte load
     const uint32_t t = blockIdx.x, tid = threadIdx.x;
-    const uint32_t tile_words32 = 1u << (tc.ts - 5);
-    const uint32_t mask = (1u << tc.ts) - 1;
-    uint32_t *shard_cnt = tile + tile_words32;  // [kShards]
+    // the tile's bits [b0, b1) (power-of-two tiles: [t << ts, (t + 1) << ts)), held in
+    // LDS from the filter word holding b0 on: LDS bit i is filter bit a0 + i
+    const uint64_t b0 = tile_start(t, tc.mul), b1 = tile_start(t + 1, tc.mul);
+    const uint64_t w0 = b0 >> 6, we = min((b1 + 63) >> 6, nwords);  // filter words [w0, we)
+    const uint32_t nw64 = (uint32_t)(we - w0), a0 = (uint32_t)(w0 << 6);
+    // an entry holds the low ts bits of its index: its LDS bit is (entry - a0) mod 2^ts
+    // (power-of-two tiles: a0's low ts bits are zero)
+    const uint32_t mask = (1u << tc.ts) - 1, abase = a0 & mask;
+    uint32_t *shard_cnt = tile + 2 * tc.w64;    // [kShards]
     uint32_t *shard_v0 = shard_cnt + kShards;   // [kShards + 1] first flat vector of each shard
-    for (uint32_t w = tid; w < tile_words32; w += NT) tile[w] = 0;
+    for (uint32_t w = tid; w < 2 * nw64; w += NT) tile[w] = 0;
     if (tid < tc.G) {
         uint32_t *cp = sc.gcur + (size_t)tid * tc.T + t;
         shard_cnt[tid] = min(*cp, tc.cap);
@@ -1357,7 +1387,7 @@ __global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
     }
     __syncthreads();
     auto orv = [&](uint32_t v) {
-        v &= mask;
+        v = (v - abase) & mask;
         atomicOr(&tile[v >> 5], 1u << (v & 31));
     };
     auto or_vec = [&](const uint4 &q) {
@@ -1402,30 +1432,38 @@ __global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
             }
         }
     }
-    const uint64_t w0 = (uint64_t)t << (tc.ts - 6);
-    const uint32_t tile_words64 = tile_words32 / 2;
     if (sc.spill_flag[t]) {  // fold in (and clear) this tile's spilled bits
         __syncthreads();
         uint32_t *sp = sc.spill32 + 2 * w0;
-        for (uint32_t w = tid; w < tile_words32; w += NT) {
-            if ((w0 * 2 + w) < 2 * nwords) {
-                const uint32_t v = sp[w];
-                if (v) {
-                    atomicOr(&tile[w], v);
-                    sp[w] = 0;
-                }
+        for (uint32_t w = tid; w < 2 * nw64; w += NT) {
+            uint32_t v = sp[w];
+            // only the bits of [b0, b1): a boundary word's others are the neighbour's
+            const uint64_t bit0 = (uint64_t)a0 + 32 * w;
+            const uint64_t lo = max(b0, bit0), hi = min(b1, bit0 + 32);
+            v = lo < hi ? v & (uint32_t)((((hi - bit0) == 32 ? 0x100000000ull : 1ull << (hi - bit0)) - 1) &
+                                         ~((1ull << (lo - bit0)) - 1))
+                        : 0u;
+            if (v) {
+                atomicOr(&tile[w], v);
+                atomicAnd(&sp[w], ~v);
             }
         }
         if (tid == 0) sc.spill_flag[t] = 0;
     }
     __syncthreads();
+    // a word holding a tile boundary (counted tiles only) is shared with the
+    // neighbour tile's block: ORed in atomically (zeroed by the bin kernel when the
+    // build overwrites); every other word is this block's alone
+    const bool lo_shared = (b0 & 63) != 0, hi_shared = t + 1 < tc.T && (b1 & 63) != 0;
     const uint64_t *tile64 = reinterpret_cast<const uint64_t *>(tile);
-    for (uint32_t w = tid; w < tile_words64; w += NT) {
-        const uint64_t gw = w0 + w;
-        if (gw < nwords) {
-            const uint64_t v = tile64[w];
-            if (OVERWRITE) words[gw] = v;
-            else if (v) words[gw] |= v;
+    for (uint32_t w = tid; w < nw64; w += NT) {
+        const uint64_t gw = w0 + w, v = tile64[w];
+        if ((w == 0 && lo_shared) || (w == nw64 - 1 && hi_shared)) {
+            if (v) __hip_atomic_fetch_or(words + gw, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (OVERWRITE) {
+            words[gw] = v;
+        } else if (v) {
+            words[gw] |= v;
         }
     }
 }
@@ -1466,7 +1504,7 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
     uint32_t *skid = sidx + NT * k;                     // [NT * k] their keys
     const uint64_t base = (uint64_t)blockIdx.x * NT;
     BinPhase1<FLAVOR, LAYOUT, 1, NT, STAGE, KR> ph;
-    ph.run(keys, offsets, key_len, n, c, tc.ts, T, cnt, sidx, wave_sums + NT / 64 + 1, base);
+    ph.run(keys, offsets, key_len, n, c, tc.mul, T, cnt, sidx, wave_sums + NT / 64 + 1, base);
     const bool valid = base + tid < n;  // (staged keys: the valid ones fill the first slots)
     if (valid) out[ph.kid[0]] = 1;
     // counts from the placement handles (A_t << kHandleShift | 4 rank, see BinPhase1)
@@ -1790,13 +1828,66 @@ TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     cap = (cap + 7) & ~7ull;
     tc.cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFC0ull);
     tc.fts = ts;
+    tc.mul = tc.fmul = pow2_mul(ts);
+    tc.w64 = 1u << (ts - 6);
     return tc;
+}
+
+// Counted tiles for the single-level packed path (TileCfg): the fewest tiles that
+// fill whole tile-kernel rounds -- a multiple of the device's CU count -- and still
+// fit one tile block's LDS (160 KiB less the shard counters: <= 1 310 048 bits with
+// the two boundary words), while the power-of-two tiling (`p2`) leaves a partial
+// last round.  NB_TILE_COUNT: 0 this policy, 1 off, N > 1 exactly N tiles.  Entries
+// then hold 21-bit in-tile offsets (ts = 21: tiles < 2^21 bits with their boundary
+// words).  C4 / C3 (m = 958 505 838): 768 tiles, three rounds, instead of 915.
+uint32_t device_cus() {
+    static std::atomic<int> cus{0};
+    int v = cus.load(std::memory_order_relaxed);
+    if (!v) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            v = 256;
+        cus.store(v, std::memory_order_relaxed);
+    }
+    return (uint32_t)v;
+}
+
+uint32_t cap_for(uint32_t T, uint32_t G, uint64_t n, uint32_t k);
+
+bool counted_tiles(uint32_t m, uint64_t n_chunk, uint32_t k, const TileCfg &p2, TileCfg *out) {
+    const uint64_t kv = knob(nb::kKnobTileCount);
+    if (kv == 1 || m < (1u << 24)) return false;
+    constexpr uint64_t kMaxBits = (160 * 1024 - (2 * kShards + 1) * 4) * 8ull - 128;
+    const uint64_t tmin = ((uint64_t)m + kMaxBits - 1) / kMaxBits;
+    uint64_t T = kv;
+    if (kv == 0) {
+        const uint32_t cus = device_cus();
+        if (p2.T <= cus || p2.T % cus == 0) return false;  // already whole rounds
+        T = (tmin + cus - 1) / cus * cus;
+        if (T >= p2.T) return false;
+    }
+    if (T < tmin || T > kMaxTiles || T >= m) return false;
+    TileCfg tc = p2;
+    tc.mul = (uint32_t)((T << 32) / m);  // floor(2^32 T / m) < 2^32
+    tc.T = (uint32_t)(((uint64_t)(m - 1) * tc.mul >> 32) + 1);
+    const uint64_t maxlen = ((1ull << 32) + tc.mul - 1) / tc.mul + 1;
+    tc.w64 = (uint32_t)((maxlen + 63) / 64 + 1);
+    tc.ts = tc.fts = 21;
+    tc.fmul = tc.mul;
+    if ((uint64_t)tc.w64 * 64 >= (1ull << 21) || (uint64_t)tc.w64 * 8 + (2 * kShards + 1) * 4 > 160 * 1024)
+        return false;
+    tc.cap = cap_for(tc.T, tc.G, n_chunk, k);
+    *out = tc;
+    return true;
 }
 
 // The same tiling at a given tile size (NB_FINE_BITS: the two-level build's fine tiles).
 TileCfg retile(const TileCfg &base, uint32_t m, uint64_t n_chunk, uint32_t k, uint32_t ts) {
     TileCfg tc = base;
     tc.ts = tc.fts = ts;
+    tc.mul = tc.fmul = pow2_mul(ts);
+    tc.w64 = 1u << (ts - 6);
     tc.T = (uint32_t)(((uint64_t)m + (1ull << ts) - 1) >> ts);
     const double e = (double)n_chunk * k / ((double)tc.T * tc.G);
     uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
@@ -1816,6 +1907,9 @@ TileCfg super_tiles(const TileCfg &fine, uint32_t m, uint64_t n_chunk, uint32_t 
     cap = (cap + 7) & ~7ull;
     tc.cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFC0ull);
     tc.fts = fine.ts;
+    tc.mul = pow2_mul(tc.ts);
+    tc.fmul = pow2_mul(fine.ts);
+    tc.w64 = 0;  // (super tiles never reach the tile kernel)
     return tc;
 }
 
@@ -1870,7 +1964,7 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     if (sizeof(ENTRY) == 8) sort_bytes += (size_t)tc.T * 8;  // <= 2 pad slots per run
     if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(NT));
     const size_t bin_lds = (size_t)bin_sort_offset_words(tc.T) * 4 + sort_bytes;
-    const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
+    const size_t tile_lds = (size_t)tc.w64 * 8 + (2 * kShards + 1) * 4;
     auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, ENTRY, NT, STAGE, KR, KX>;
     auto tile_ow = bloom_tile_or_kernel<ENTRY, true>;
     auto tile_or = bloom_tile_or_kernel<ENTRY, false>;
@@ -1883,8 +1977,11 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         const uint64_t cn = std::min(chunk, n - done);
         const uint8_t *ck = offsets ? keys : keys + done * key_len;
         const uint64_t *co = offsets ? offsets + done : nullptr;
+        TileScratch scb = sc;  // counted tiles, overwrite: the bin kernel zeroes the
+                               // boundary words the tile kernel ORs into
+        scb.zero_words = overwrite && done == 0 && tc.mul != pow2_mul(tc.ts) ? words : nullptr;
         hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st, ck,
-                           co, key_len, cn, c, tc, sc, bk);
+                           co, key_len, cn, c, tc, scb, bk);
         NB_HIP(hipGetLastError());
         hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(tc.T),
                            dim3(kTileThreads), tile_lds, st, tc, sc, bk, words, nwords);
@@ -1972,7 +2069,7 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
     if (STAGE) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(NT));
     const size_t bin_lds = (size_t)bin_sort_offset_words(t1.T) * 4 + sort_bytes;
     const size_t rebin_lds = ((size_t)rebin_span<IN5>() + 2 * kSuperFine) * 4;
-    const size_t tile_lds = ((size_t)1 << (t2.ts - 3)) + (2 * kShards + 1) * 4;
+    const size_t tile_lds = (size_t)t2.w64 * 8 + (2 * kShards + 1) * 4;
     auto bin = bloom_bin_kernel<FLAVOR, LAYOUT, KPT, E1, NT, STAGE, KR, KX>;
     auto rebin = pack ? bloom_rebin_kernel<true, IN5> : bloom_rebin_kernel<false, IN5>;
     auto tile_ow = pack ? tile_kernel_of<uint64_t, true>() : tile_kernel_of<uint32_t, true>();
@@ -2088,10 +2185,16 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
         // ... only while two bin blocks still fit a CU's LDS with the pad slots (up to
         // T ~ 1 100: packed C4 at 2^19-bit tiles, T = 1 829, ran 2.47 vs 2.30 ms with
         // one block per CU)
-        size_t pk_lds = (size_t)kpb * c.k * 4 + (size_t)tc.T * 8;
-        if (STAGE) pk_lds = std::max<size_t>(pk_lds, stage_lds_bytes(NT));
-        pk_lds += (size_t)bin_sort_offset_words(tc.T) * 4;
-        if (tc.ts <= 20 && tc.T <= 2u * NT && NB_TWO_TILE && pk_lds <= 80 * 1024 &&
+        auto pk_lds_of = [&](uint32_t T) {
+            size_t b = (size_t)kpb * c.k * 4 + (size_t)T * 8;
+            if (STAGE) b = std::max<size_t>(b, stage_lds_bytes(NT));
+            return b + (size_t)bin_sort_offset_words(T) * 4;
+        };
+        TileCfg ct;
+        if (tc.ts <= 20 && counted_tiles(c.fm.m, chunk, c.k, tc, &ct) && ct.T <= 2u * NT &&
+            pk_lds_of(ct.T) <= 80 * 1024)
+            tc = ct;
+        if (tc.ts <= 21 && tc.T <= 2u * NT && NB_TWO_TILE && pk_lds_of(tc.T) <= 80 * 1024 &&
             knob(nb::kKnobPack) != 0) {
             const uint64_t nblk = (chunk + kpb - 1) / kpb;
             const uint64_t bps = (nblk + tc.G - 1) / tc.G;
@@ -2222,6 +2325,8 @@ TileCfg probe_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
     tc.cap = (uint32_t)std::min<uint64_t>((cap + 7) & ~7ull, 0xFFFFFFC0ull);
     tc.fts = ts;
+    tc.mul = tc.fmul = pow2_mul(ts);
+    tc.w64 = 1u << (ts - 6);
     return tc;
 }
 

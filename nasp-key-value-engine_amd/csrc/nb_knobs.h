@@ -45,6 +45,9 @@ enum Knob : int {
     kKnobSubpasses,     // NB_SUBPASSES      bin + re-bin sub-passes per tile pass (2)
     kKnobFineBits,      // NB_FINE_BITS      0: fine-tile policy (2^20 bits); 19: 2^19-bit fine
                         //                   tiles in the two-level build
+    kKnobTileCount,     // NB_TILE_COUNT     0: counted-tile policy (single-level packed path:
+                        //                   a whole number of tile-kernel rounds), 1:
+                        //                   power-of-two tiles only, else that many tiles
     kKnobProbePath,     // NB_PROBE_PATH     0 auto | 1 "lane" (one lane per key) | 2 "tiled"
     kKnobFailBuilds,    // NB_FAIL_BUILDS    fault injection: the next N device builds fail
                         //                   with NB_ERR_HIP before launching anything

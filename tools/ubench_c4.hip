@@ -10,13 +10,17 @@
 //   3. the tile kernel and the bin kernel restricted to x CUs by a stream CU mask;
 //   4. a chunked pipeline: bin kernels on (256 - x) CUs beside tile kernels on x
 //      CUs, checked bit for bit against the one-shot build.
-// usage: ubench_c4 [all|stops|mask|pipe]
+//   5. power-of-two (915) vs counted (768) tiles, one-shot builds interleaved.
+// usage: ubench_c4 [all|stops|tiles|mask|pipe]
 #include <hip/hip_runtime.h>
 __constant__ int g_diag_stop;
 #define NB_DIAG_STOP(phase) (g_diag_stop == (phase) || ((phase) == 1 && g_diag_stop == 11))
 #define NB_DIAG_NOCOUNT (g_diag_stop == 11)
 #include "../nasp-key-value-engine_amd/csrc/bloom_kernels.hip"
 
+#include <unistd.h>
+
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -97,6 +101,22 @@ static void launch_tile(Setup &s, int q, const TileCfg &tc, bool ow, uint64_t *w
                        ((uint64_t)kM + 63) / 64);
 }
 
+// wait for a stream with a deadline: a CU mask that selects no usable CU would
+// leave the launch pending forever -- report it and leave without tearing down
+static void wait_or_die(hipStream_t s, const char *what, double secs = 5.0) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (true) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) { printf("HIP error %s waiting for %s\n", hipGetErrorString(q), what); _exit(4); }
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > secs) {
+            printf("TIMEOUT: %s did not complete in %.0f s\n", what, secs);
+            _exit(3);
+        }
+        usleep(200);
+    }
+}
+
 struct Ev {
     hipEvent_t a, b;
     Ev() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
@@ -128,7 +148,7 @@ static void where(int x, int mode) {
     CK(hipFuncSetAttribute(reinterpret_cast<const void *>(k_where),
                            hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024));
     hipLaunchKernelGGL(k_where, dim3(nb), dim3(64), 100 * 1024, s, d);
-    CK(hipStreamSynchronize(s));
+    wait_or_die(s, "k_where on a masked stream");
     std::vector<uint32_t> h(nb);
     CK(hipMemcpy(h.data(), d, nb * 4, hipMemcpyDeviceToHost));
     std::map<uint32_t, int> cu;
@@ -143,6 +163,7 @@ static void where(int x, int mode) {
 }
 
 int main(int argc, char **argv) {
+    setvbuf(stdout, nullptr, _IONBF, 0);
     const char *what = argc > 1 ? argv[1] : "all";
     const bool all = !strcmp(what, "all");
     Setup s;
@@ -236,7 +257,68 @@ int main(int argc, char **argv) {
         }
     }
 
+    if (all || !strcmp(what, "tiles")) {
+        // power-of-two tiles (915) vs counted tiles (768: three tile-kernel rounds),
+        // one-shot builds interleaved, both checked against the reference filter
+        TileCfg p2 = choose_tiles(kM, kN, kK), ct;
+        if (!counted_tiles(kM, kN, kK, p2, &ct)) { printf("counted tiles: policy declined\n"); return 1; }
+        {
+            const uint64_t nblk = (kN + kKPB - 1) / kKPB, bps = (nblk + ct.G - 1) / ct.G;
+            const uint64_t capw = ((uint64_t)ct.cap + 2 * bps + 2) / 3;
+            ct.cap = (uint32_t)((capw + 7) & ~7ull);
+        }
+        CK(hipFuncSetAttribute(reinterpret_cast<const void *>(BIN), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)std::max(bin_lds_of(tfull), bin_lds_of(ct))));
+        for (auto k : {bloom_tile_or_kernel<uint64_t, true, kTileThreads, 4>})
+            CK(hipFuncSetAttribute(reinterpret_cast<const void *>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)(ct.w64 * 8 + (2 * kShards + 1) * 4)));
+        printf("counted: T=%u mul=%u w64=%u cap=%u, tile LDS %u B, bin LDS %zu B\n", ct.T, ct.mul, ct.w64, ct.cap,
+               ct.w64 * 8 + (2 * kShards + 1) * 4, bin_lds_of(ct));
+        float bb[2] = {1e30f, 1e30f}, tt[2] = {1e30f, 1e30f}, sum[2] = {0, 0};
+        for (int r = 0; r < 8; ++r)
+            for (int v = 0; v < 2; ++v) {
+                const TileCfg &tc = v ? ct : tfull;
+                TileScratch sc = s.sc[0];
+                sc.zero_words = v ? s.words : nullptr;
+                CK(hipMemsetAsync(s.words, 0xA5, nwords * 8, s0));
+                Ev e, f;
+                CK(hipEventRecord(e.a, s0));
+                hipLaunchKernelGGL(BIN, dim3((uint32_t)((kN + kKPB - 1) / kKPB)), dim3(kNT), bin_lds_of(tc), s0,
+                                   s.keys, nullptr, 16u, kN, s.c, tc, sc, s.bk[0]);
+                CK(hipEventRecord(e.b, s0));
+                CK(hipEventRecord(f.a, s0));
+                hipLaunchKernelGGL((bloom_tile_or_kernel<uint64_t, true, kTileThreads, 4>), dim3(tc.T),
+                                   dim3(kTileThreads), (size_t)tc.w64 * 8 + (2 * kShards + 1) * 4, s0, tc,
+                                   s.sc[0], s.bk[0], s.words, nwords);
+                CK(hipEventRecord(f.b, s0));
+                const float b = e.ms(), t = f.ms();
+                bb[v] = std::min(bb[v], b);
+                tt[v] = std::min(tt[v], t);
+                if (r >= 2) sum[v] += b + t;
+                if (r == 7) {
+                    std::vector<uint64_t> a(nwords), ref(nwords);
+                    CK(hipMemcpy(a.data(), s.words, nwords * 8, hipMemcpyDeviceToHost));
+                    CK(hipMemcpy(ref.data(), s.words_ref, nwords * 8, hipMemcpyDeviceToHost));
+                    printf("%s tiles: %s\n", v ? "counted" : "pow2", a == ref ? "bit-exact" : "MISMATCH");
+                }
+            }
+        for (int v = 0; v < 2; ++v)
+            printf("%s tiles (T=%u): bin best %.4f, tile best %.4f, build mean(6) %.4f ms\n", v ? "counted" : "pow2",
+                   v ? ct.T : tfull.T, bb[v], tt[v], sum[v] / 6);
+    }
+
     if (all || !strcmp(what, "mask")) {
+        {
+            hipStream_t d;
+            CK(hipStreamCreateWithFlags(&d, hipStreamNonBlocking));
+            uint32_t m[16] = {0};
+            CK(hipExtStreamGetCUMask(d, 16, m));
+            int bits = 0;
+            printf("default stream CU mask:");
+            for (int i = 0; i < 16; ++i) { printf(" %08x", m[i]); bits += __builtin_popcount(m[i]); }
+            printf("  (%d bits)\n", bits);
+            CK(hipStreamDestroy(d));
+        }
         for (int x : {32, 64, 128}) {
             where(x, 0);
             where(x, 1);
@@ -253,6 +335,7 @@ int main(int argc, char **argv) {
                 CK(hipEventRecord(e.a, sm));
                 launch_tile<4>(s, 0, tfull, true, s.words, sm);
                 CK(hipEventRecord(e.b, sm));
+                wait_or_die(sm, "tile kernel on a masked stream");
                 t4 = std::min(t4, e.ms());
                 launch_bin(s, 0, tfull, 0, kN, s0);
                 CK(hipStreamSynchronize(s0));
@@ -260,6 +343,7 @@ int main(int argc, char **argv) {
                 CK(hipEventRecord(f.a, sm));
                 launch_tile<16>(s, 0, tfull, true, s.words, sm);
                 CK(hipEventRecord(f.b, sm));
+                wait_or_die(sm, "tile kernel on a masked stream");
                 t16 = std::min(t16, f.ms());
             }
             printf("tile kernel on %3d CUs: unroll 4 %.4f ms, unroll 16 %.4f ms\n", x, t4, t16);
@@ -273,6 +357,7 @@ int main(int argc, char **argv) {
                 CK(hipEventRecord(e.a, sm));
                 launch_bin(s, 0, tfull, 0, kN, sm);
                 CK(hipEventRecord(e.b, sm));
+                wait_or_die(sm, "bin kernel on a masked stream");
                 best = std::min(best, e.ms());
                 launch_tile(s, 0, tfull, true, s.words, sm);
             }
@@ -331,6 +416,7 @@ int main(int argc, char **argv) {
                     }
                     CK(hipStreamWaitEvent(s0, ev_tile[(c - 1) & 1], 0));
                     CK(hipEventRecord(e.b, s0));
+                    wait_or_die(s0, "the chunked pipeline", 10.0);
                     best = std::min(best, e.ms());
                     if (r == 3) {
                         std::vector<uint64_t> a(nwords), b(nwords);
