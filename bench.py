@@ -274,6 +274,28 @@ def valu_frac_of(sq):
     return round(sum(v["valu_floor_us"] for v in ks) / sum(v["avg_duration_us"] for v in ks), 4)
 
 
+def steady_state(step, stream, dev, n):
+    """Diagnostic beside `value`, never it: n more builds right after the timed ones,
+    each bracketed by its own HIP events on the build stream.  The build time follows
+    the chip's clock, which the power controller pulls down for the first ~25 builds
+    after any idle gap and then raises again (profiles/r04_c4_dispatch_clock.txt,
+    DESIGN.md §6): the timed K steps after W warmup steps sit in that ramp, the last
+    builds here show the settled rate."""
+    import torch
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
+    evs[0].record(stream)
+    for i in range(n):
+        step()
+        evs[i + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(n)]
+    last = ms[-20:]
+    return {"build_ms": [round(x, 4) for x in ms], "last20_mean_ms": round(sum(last) / len(last), 5),
+            "last20_min_ms": round(min(last), 5),
+            "note": "per-build device time of 40 builds after the timed steps (events per build); "
+                    "the build time tracks the DVFS clock -- not the contract value"}
+
+
 def rank_diag(per_rank, key):
     """N > 1 self-diagnosis: the world size and the backend the
     process group reports, each rank's own numbers, and the min / max of `key`."""
@@ -321,6 +343,8 @@ def main():
                     help="skip the host-buffer (H2D + build + D2H) rate measurement")
     ap.add_argument("--no-probe", action="store_true", help="skip the batch-probe rates")
     ap.add_argument("--no-c2", action="store_true", help="skip the extra C2 line of the c4 run")
+    ap.add_argument("--no-steady", action="store_true",
+                    help="skip the per-build steady-state series after the timed steps")
     ap.add_argument("--no-rank-share", action="store_true",
                     help="c5 at N=1: skip the per-rank (1B/8 keys) partial-build line")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -437,6 +461,8 @@ def main():
            "roofline": roofline}
     if ranks is not None:
         out["ranks"] = ranks
+    if world == 1 and not args.no_steady:
+        out["steady_state"] = steady_state(step, stream, dev, 40)
     if rank == 0 and world == 1 and args.workload == "c4" and not args.no_c2:
         out["c2"] = c2_rate(nbm, synth, dev, stream, args.flavor)
     if rank == 0 and world == 1 and not args.no_probe:

@@ -17,7 +17,7 @@ WL=${2:-c4}
 OUT=gpurun_out/prof_${TAG}_${WL}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-B="python3 bench.py --workload $WL --no-cpu-baseline --no-host-path --no-probe --no-c2 --no-rank-share --steps 10 --warmup 2"
+B="python3 bench.py --workload $WL --no-cpu-baseline --no-host-path --no-probe --no-c2 --no-rank-share --no-steady --steps 10 --warmup 2"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o run --output-format csv -- $B > "$OUT/bench_trace.json" 2> "$OUT/trace.err" || exit 1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/fetch" -o run --output-format csv -- $B > /dev/null 2> "$OUT/fetch.err" || exit 2
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/write" -o run --output-format csv -- $B > /dev/null 2> "$OUT/write.err" || exit 3
