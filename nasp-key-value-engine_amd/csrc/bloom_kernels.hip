@@ -1195,6 +1195,199 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     }
 }
 
+// Pipelined bin kernel (round 4) for 16-byte keys at k = KX with packed entries and
+// T <= 1 024 tiles (C4's shape).  The two-blocks-per-CU bin kernel runs its phases
+// one after the other in each block -- hash + count (VALU), scan + reservations,
+// placement (LDS), write-out (HBM stores) -- and the 512 resident blocks start
+// together, so the chip's write-outs bunch up.  Here one persistent 1 024-thread
+// block per CU holds two batches of 2 304 keys in LDS and overlaps them:
+//   A  waves 0-11 (H, 768 threads x 3 keys) hash batch i and count its indices into
+//      buffer i & 1, while waves 12-15 (S) write batch i-1's runs out of the other
+//      buffer;
+//   B  all 16 waves scan batch i's counts (one tile per thread) and reserve its runs;
+//   C  H places batch i; S resets the other buffer for batch i+1 (counters, run-pad
+//      sentinels, flags); each tile's owner writes its run table entry.
+// Run pads need no pass of their own: the sort area is filled with a sentinel
+// (0xFFFFFFFF, never an index) before the placement, and the write-out replaces a
+// sentinel slot by the first slot of its word (always a real entry of the same run).
+// The buckets, cursors and spill handling are the bin kernel's, so the tile kernel
+// is unchanged.  Four LDS-only barriers per batch (the write-out's stores stay in
+// flight across them).
+constexpr int kPipeThreads = 1024, kPipeH = 768, kPipeKPT = 3;
+constexpr uint32_t kPipeKPB = (uint32_t)kPipeH * kPipeKPT;  // keys per batch
+constexpr uint32_t kPipeMaxT = kPipeThreads;
+constexpr uint32_t kPipeMisc = 32;  // per buffer: [0, 16) wave sums, [16] slots, [17] overflow
+constexpr uint32_t kSortSentinel = 0xFFFFFFFFu;
+__host__ __device__ constexpr uint32_t pipe_sort_off(uint32_t T) { return (4 * T + 2 * kPipeMisc + 3) & ~3u; }
+__host__ __device__ constexpr uint32_t pipe_sort_words(uint32_t T, uint32_t kx) {
+    return (kPipeKPB * kx + 2 * T + 3) & ~3u;
+}
+__host__ __device__ constexpr size_t pipe_lds_bytes(uint32_t T, uint32_t kx) {
+    return ((size_t)pipe_sort_off(T) + 2 * (size_t)pipe_sort_words(T, kx)) * 4;
+}
+
+template <int FLAVOR, int KX>
+__global__ __launch_bounds__(kPipeThreads, 1) void bloom_bin_pipe_kernel(
+    const uint8_t *__restrict__ keys, uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc,
+    uint64_t *__restrict__ buckets) {
+    extern __shared__ uint32_t lds[];
+    const uint32_t T = tc.T, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const bool isH = tid < (uint32_t)kPipeH;
+    const uint32_t sort_off = pipe_sort_off(T), sort_words = pipe_sort_words(T, KX);
+    auto cnt_of = [&](uint32_t q) { return lds + q * T; };
+    auto gx_of = [&](uint32_t q) { return lds + (2 + q) * T; };
+    auto misc_of = [&](uint32_t q) { return lds + 4 * T + q * kPipeMisc; };
+    auto sort_of = [&](uint32_t q) { return lds + sort_off + q * sort_words; };
+    const uint32_t shard = blockIdx.x & (tc.G - 1);
+    uint32_t *cur = sc.gcur + (size_t)shard * T;
+    const uint64_t nbatch = (n + kPipeKPB - 1) / kPipeKPB;
+    const uint32_t nit = blockIdx.x < nbatch ? (uint32_t)((nbatch - blockIdx.x + gridDim.x - 1) / gridDim.x) : 0u;
+    if (sc.zero_words && tid == 0)  // counted tiles, overwrite: see TileCfg
+        for (uint32_t t = blockIdx.x + 1; t < T; t += gridDim.x) {
+            const uint64_t b = tile_start(t, tc.mul);
+            if (b & 63) sc.zero_words[b >> 6] = 0;
+        }
+    // buffer reset for a new batch: placement-handle counters, sentinels, flags
+    auto reset = [&](uint32_t q, uint32_t t0, uint32_t nthr) {
+        uint32_t *cq = cnt_of(q);
+        for (uint32_t t = t0; t < T; t += nthr) cq[t] = lds_addr(cq + t) << kHandleShift;
+        uint4 *s4 = reinterpret_cast<uint4 *>(sort_of(q));
+        const uint4 sent = make_uint4(kSortSentinel, kSortSentinel, kSortSentinel, kSortSentinel);
+        for (uint32_t w = t0; w < sort_words / 4; w += nthr) s4[w] = sent;
+        if (t0 == 0) misc_of(q)[17] = 0u;
+    };
+    reset(0, tid, kPipeThreads);
+    lds_barrier();
+
+    KeyBatch<FLAVOR, kFixed16, kPipeKPT> kb;
+    uint32_t ridx[kPipeKPT][KX], rank[kPipeKPT][KX];
+    auto batch_base = [&](uint32_t it) { return (uint64_t)(blockIdx.x + (uint64_t)it * gridDim.x) * kPipeKPB; };
+    if (isH && nit) kb.load(keys, nullptr, batch_base(0) + tid, kPipeH, n);
+    const uint32_t msk = (1u << tc.ts) - 1, hb = tc.ts - 11;
+    for (uint32_t it = 0; it <= nit; ++it) {
+        const uint32_t q = it & 1, p = q ^ 1;
+        const bool have = it < nit;
+        const uint64_t base = have ? batch_base(it) : 0;
+        // ---- A: H hashes + counts batch it into buffer q; S writes batch it-1 out of p
+        if (isH) {
+            if (have) {
+                uint32_t *cq = cnt_of(q);
+                uint64_t h1[kPipeKPT], h2[kPipeKPT];
+#pragma unroll
+                for (int k2 = 0; k2 < kPipeKPT; ++k2)
+                    kb.hash(c, keys, 16, base + (uint64_t)k2 * kPipeH + tid, k2, &h1[k2], &h2[k2]);
+#pragma unroll
+                for (int k2 = 0; k2 < kPipeKPT; ++k2)
+                    if (base + (uint64_t)k2 * kPipeH + tid < n) {
+                        IndexGen g;
+                        g.start(h1[k2], h2[k2], c);
+#pragma unroll
+                        for (int j = 0; j < KX; ++j) {
+                            if (j) g.next(c);
+                            ridx[k2][j] = g.r;
+                            rank[k2][j] = atomicAdd(&cq[__umulhi(g.r, tc.mul)], 4u);
+                        }
+                    }
+            }
+        } else if (it > 0) {
+            const uint32_t *sp = sort_of(p), *gp = gx_of(p), *mp = misc_of(p);
+            const uint32_t words = mp[16] / 3;
+            const bool ovf = mp[17] != 0u;
+            char *bb = reinterpret_cast<char *>(buckets);
+            for (uint32_t w = tid - kPipeH; w < words; w += kPipeThreads - kPipeH) {
+                const uint32_t a = sp[3 * w];
+                uint32_t b = sp[3 * w + 1], cc = sp[3 * w + 2];
+                b = b == kSortSentinel ? a : b;  // run pads: copies of the word's first entry
+                cc = cc == kSortSentinel ? a : cc;
+                const uint32_t t = __umulhi(a, tc.mul);
+                if (t >= T) continue;  // never (a word's first slot is a placed entry): no wild store
+                const uint32_t g = gp[t];
+                const uint32_t lo = (a & msk) | (b << 21);
+                const uint32_t hi = __builtin_amdgcn_ubfe(b, 11, hb) | ((cc & msk) << 10);
+                const uint64_t word = (uint64_t)hi << 32 | lo;
+                if (!ovf) {
+                    bucket_store(reinterpret_cast<uint64_t *>(bb + (g + w * 8u)), word);
+                } else {
+                    // pathological duplicates: a word past its bucket's capacity goes to
+                    // the spill bitmap (its position in the bucket from the run table)
+                    const uint32_t pos = (g + w * 8u) / 8u - (t * tc.G + shard) * tc.cap;
+                    if (pos < tc.cap) {
+                        bucket_store(reinterpret_cast<uint64_t *>(bb + (g + w * 8u)), word);
+                    } else {
+                        const uint32_t v3[3] = {a, b, cc};
+                        for (int r = 0; r < 3; ++r) {
+                            __hip_atomic_fetch_or(sc.spill32 + (v3[r] >> 5), 1u << (v3[r] & 31), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+                            sc.spill_flag[__umulhi(v3[r], tc.fmul)] = 1u;
+                        }
+                    }
+                }
+            }
+        }
+        lds_barrier();
+        if (!have) break;  // block-uniform: the last batch is written out
+        // ---- B: scan batch it's counts (thread t owns tile t), reserve its runs
+        uint32_t *cq = cnt_of(q), *mq = misc_of(q);
+        const uint32_t t = tid;
+        uint32_t h = 0;
+        if (t < T) h = (cq[t] - (lds_addr(cq + t) << kHandleShift)) >> 2;
+        const uint32_t local = (h + 2) / 3 * 3, incl = wave_inclusive_scan(local);
+        if (lane == 63) mq[wid] = incl;
+        lds_barrier();
+        const uint32_t wv = lane < kPipeThreads / 64 ? mq[lane] : 0u;
+        uint32_t before = lane < wid ? wv : 0u, all = wv;
+#pragma unroll
+        for (int o = 32; o; o >>= 1) {
+            before += __shfl_xor(before, o);
+            all += __shfl_xor(all, o);
+        }
+        const uint32_t st = before + incl - local;  // run start (slots)
+        const uint32_t u = (h + 2) / 3;             // run words
+        uint32_t ga = 0;
+        if (t < T) {
+            cq[t] = lds_addr(sort_of(q)) + 4 * st;
+            if (u) ga = atomicAdd(&cur[t], u);
+        }
+        if (tid == 0) mq[16] = all;
+        lds_barrier();
+        // ---- C: H places batch it; S resets buffer p for batch it+1; owners write
+        // the run table; H prefetches batch it+1's keys
+        if (isH) {
+            if (it + 1 < nit) {
+                KeyBatch<FLAVOR, kFixed16, kPipeKPT> nk;
+                nk.load(keys, nullptr, batch_base(it + 1) + tid, kPipeH, n);
+#pragma unroll
+                for (int k2 = 0; k2 < kPipeKPT; ++k2)
+                    if (base + (uint64_t)k2 * kPipeH + tid < n) {
+                        uint32_t s[KX];
+#pragma unroll
+                        for (int j = 0; j < KX; ++j) s[j] = lds_at(rank[k2][j] >> kHandleShift);
+#pragma unroll
+                        for (int j = 0; j < KX; ++j) lds_at(s[j] + (rank[k2][j] & kHandleMask)) = ridx[k2][j];
+                    }
+                kb = nk;
+            } else {
+#pragma unroll
+                for (int k2 = 0; k2 < kPipeKPT; ++k2)
+                    if (base + (uint64_t)k2 * kPipeH + tid < n) {
+                        uint32_t s[KX];
+#pragma unroll
+                        for (int j = 0; j < KX; ++j) s[j] = lds_at(rank[k2][j] >> kHandleShift);
+#pragma unroll
+                        for (int j = 0; j < KX; ++j) lds_at(s[j] + (rank[k2][j] & kHandleMask)) = ridx[k2][j];
+                    }
+            }
+        } else {
+            reset(p, tid - kPipeH, kPipeThreads - kPipeH);
+        }
+        if (t < T) {
+            gx_of(q)[t] = ((t * tc.G + shard) * tc.cap + ga - st / 3) * 8u;
+            if ((uint64_t)ga + u > tc.cap) mq[17] = 1u;
+        }
+        lds_barrier();
+    }
+}
+
 // Two-level build for very large filters (T > 2 NT fine tiles, e.g. C5's 4 096
 // tiles of 2^20 bits): binned straight into fine tiles, a block's 1 024 keys x k
 // indices spread over T tiles make runs of ~2.5 entries -- every run a separate
@@ -1971,6 +2164,22 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(tile_ow, tile_lds)) ||
         (rc = allow_lds(tile_or, tile_lds)))
         return rc;
+    // the pipelined bin kernel for its shape (bloom_bin_pipe_kernel): 16-byte keys at
+    // k = KX, packed entries, batches of the same 2 304 keys (so the capacity the
+    // caller sized per block holds per batch), 385..1 024 tiles, buckets < 4 GiB
+    bool pipe = false;
+    uint32_t pipe_grid = 0;
+    const size_t pipe_lds = pipe_lds_bytes(tc.T, KX > 0 ? KX : 1);
+    if constexpr (LAYOUT == kFixed16 && sizeof(ENTRY) == 8 && KX > 0 && (uint64_t)KPT * NT == kPipeKPB) {
+        pipe = knob(nb::kKnobBinPipe) != 0 && tc.T <= kPipeMaxT && tc.T > kThreeBlockTiles &&
+               (uint64_t)tc.T * tc.G * tc.cap * sizeof(ENTRY) <= 0xFFFFFFFFull && pipe_lds <= 160 * 1024;
+        if (pipe) {
+            auto pk = bloom_bin_pipe_kernel<FLAVOR, KX>;
+            NB_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(pk),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)pipe_lds));
+            pipe_grid = device_cus();
+        }
+    }
     const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
     ENTRY *bk = reinterpret_cast<ENTRY *>(ws->buckets);
     for (uint64_t done = 0; done < n; done += chunk) {
@@ -1980,8 +2189,17 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         TileScratch scb = sc;  // counted tiles, overwrite: the bin kernel zeroes the
                                // boundary words the tile kernel ORs into
         scb.zero_words = overwrite && done == 0 && tc.mul != pow2_mul(tc.ts) ? words : nullptr;
-        hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st, ck,
-                           co, key_len, cn, c, tc, scb, bk);
+        if constexpr (LAYOUT == kFixed16 && sizeof(ENTRY) == 8 && KX > 0 && (uint64_t)KPT * NT == kPipeKPB) {
+            if (pipe) {
+                const uint64_t nbatch = (cn + kPipeKPB - 1) / kPipeKPB;
+                hipLaunchKernelGGL((bloom_bin_pipe_kernel<FLAVOR, KX>),
+                                   dim3((uint32_t)std::min<uint64_t>(nbatch, pipe_grid)), dim3(kPipeThreads),
+                                   pipe_lds, st, ck, cn, c, tc, scb, reinterpret_cast<uint64_t *>(bk));
+            }
+        }
+        if (!pipe)
+            hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st, ck,
+                               co, key_len, cn, c, tc, scb, bk);
         NB_HIP(hipGetLastError());
         hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(tc.T),
                            dim3(kTileThreads), tile_lds, st, tc, sc, bk, words, nwords);

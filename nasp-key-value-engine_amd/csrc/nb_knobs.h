@@ -48,6 +48,8 @@ enum Knob : int {
     kKnobTileCount,     // NB_TILE_COUNT     0: counted-tile policy (single-level packed path:
                         //                   a whole number of tile-kernel rounds), 1:
                         //                   power-of-two tiles only, else that many tiles
+    kKnobBinPipe,       // NB_BIN_PIPE       1: the pipelined bin kernel for 16-byte keys at
+                        //                   k = 7 over 385-1 024 tiles (C4); 0: off
     kKnobProbePath,     // NB_PROBE_PATH     0 auto | 1 "lane" (one lane per key) | 2 "tiled"
     kKnobFailBuilds,    // NB_FAIL_BUILDS    fault injection: the next N device builds fail
                         //                   with NB_ERR_HIP before launching anything

@@ -59,9 +59,12 @@ def main():
                 if wl == "c5r":
                     ms = d["per_rank_at_8"]["ms"]
                 table.setdefault((wl, label), []).append(ms)
+                ss = d.get("steady_state", {}).get("last20_mean_ms")
+                if ss is not None:
+                    table.setdefault((wl, label + "/settled"), []).append(ss)
                 print(f"rep {rep} {wl:3s} {label:14s} {ms:.4f} ms  {d['value']:.0f} Mkeys/s "
-                      f"frac {d['roofline']['frac']:.4f}", flush=True)
-    print("summary (kernel ms per build, each rep):")
+                      f"frac {d['roofline']['frac']:.4f}" + (f"  settled {ss:.4f} ms" if ss else ""), flush=True)
+    print("summary (kernel ms per build, each rep; /settled: bench steady_state last-20 mean):")
     for (wl, label), v in sorted(table.items()):
         print(f"  {wl:3s} {label:14s} " + " ".join(f"{x:.4f}" for x in v) + f"   min {min(v):.4f}")
 
