@@ -85,7 +85,7 @@ uint64_t nb_device_merkle_count(void);
  * priority, +4 tile kernels beside the next pass's bin kernel; default 6),
  * NB_SUBPASSES (bin + re-bin sub-passes per tile pass, default 2), NB_FINE_BITS,
  * NB_TILE_COUNT (0 counted-tile policy, 1 power-of-two tiles only, else that many),
- * NB_BIN_PIPE (the pipelined bin kernel for C4's shape),
+ * NB_BIN_PIPE (the pipelined bin kernel for C4's shape), NB_BIN_MIX (bin blocks of two sizes),
  * NB_SHARDED_STAGE, NB_FAIL_BUILDS / NB_FAIL_MERKLES (the next N device builds /
  * trees fail with NB_ERR_HIP).
  * Unknown names: NB_ERR_ARG. */

@@ -336,6 +336,7 @@ struct TileCfg {
     uint32_t mul;    // tile of r = __umulhi(r, mul)
     uint32_t fmul;   // spill-flag tile of r = __umulhi(r, fmul) (the fts tiling)
     uint32_t w64;    // LDS words (u64) of one tile in the tile kernel, boundary words incl.
+    uint32_t mix = 0;  // bin kernel (KPT = 3, packed): blocks of two sizes, see bin_block_keys
 };
 
 __host__ __device__ inline uint64_t tile_start(uint32_t t, uint32_t mul) {
@@ -993,6 +994,23 @@ struct BinPhase1 {
     }
 };
 
+// Blocks of two sizes (NB_BIN_MIX, KPT = 3): in every 16 consecutive blocks -- two
+// per XCD under round-robin dispatch -- the first 8 take KPT * NT keys and the last 8
+// (KPT - 1) * NT, so the two blocks resident on a CU run for different times and
+// their phases (hash, counting sort, write-out) drift apart instead of keeping step.
+// Returns the block's first key and trims *n to its last one.
+template <int KPT, int NT>
+__device__ __forceinline__ uint64_t bin_block_keys(uint32_t b, uint64_t *n) {
+    constexpr uint64_t big = (uint64_t)KPT * NT, small = (uint64_t)(KPT - 1) * NT;
+    const uint32_t g = b >> 4, r = b & 15;
+    const uint64_t base = (uint64_t)g * 8 * (big + small) + (r < 8 ? r * big : 8 * big + (r - 8) * small);
+    *n = min(*n, base + (r < 8 ? big : small));
+    return base;
+}
+__host__ __device__ constexpr uint64_t bin_mix_blocks(uint64_t n, uint64_t big, uint64_t small) {
+    return 16 * ((n + 8 * (big + small) - 1) / (8 * (big + small)));
+}
+
 // Two resident blocks per CU (8 waves per SIMD at NT = 1024): <= 64 VGPRs.
 #ifndef NB_BIN_MIN_WAVES
 #define NB_BIN_MIN_WAVES(NT) (2 * (NT) / 256)
@@ -1026,7 +1044,11 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     // low 18 bits and the decode (cnt[t] - (A_t << 18)) >> 2 is exact.
     // register-loaded keys: their loads are issued first, in flight across the LDS
     // initialisation and its barrier
-    const uint64_t base = (uint64_t)blockIdx.x * (KPT * NT);
+    uint64_t base = (uint64_t)blockIdx.x * (KPT * NT);
+    if (KPT == 3 && tc.mix) {  // blocks of two sizes (NB_BIN_MIX): see bin_block_keys
+        base = bin_block_keys<KPT, NT>(blockIdx.x, &n);
+        if (base >= n) return;
+    }
     constexpr int kR = KR > 0 ? KR : 1;
     BinPhase1<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, KX> ph;
     ph.run(keys, offsets, key_len, n, c, tc.mul, T, cnt, sorted, wave_sums + NT / 64 + 1, base);
@@ -2198,8 +2220,9 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
             }
         }
         if (!pipe)
-            hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st, ck,
-                               co, key_len, cn, c, tc, scb, bk);
+            hipLaunchKernelGGL(bin,
+                               dim3((uint32_t)(tc.mix ? bin_mix_blocks(cn, kpb, kpb - NT) : (cn + kpb - 1) / kpb)),
+                               dim3(NT), bin_lds, st, ck, co, key_len, cn, c, tc, scb, bk);
         NB_HIP(hipGetLastError());
         hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(tc.T),
                            dim3(kTileThreads), tile_lds, st, tc, sc, bk, words, nwords);
@@ -2414,10 +2437,11 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
             tc = ct;
         if (tc.ts <= 21 && tc.T <= 2u * NT && NB_TWO_TILE && pk_lds_of(tc.T) <= 80 * 1024 &&
             knob(nb::kKnobPack) != 0) {
-            const uint64_t nblk = (chunk + kpb - 1) / kpb;
+            TileCfg tp = tc;
+            tp.mix = KPT == 3 && knob(nb::kKnobBinMix) != 0 ? 1u : 0u;
+            const uint64_t nblk = tp.mix ? bin_mix_blocks(chunk, kpb, kpb - NT) : (chunk + kpb - 1) / kpb;
             const uint64_t bps = (nblk + tc.G - 1) / tc.G;
             const uint64_t capw = ((uint64_t)tc.cap + 2 * bps + 2) / 3;
-            TileCfg tp = tc;
             tp.cap = (uint32_t)std::min<uint64_t>((capw + 7) & ~7ull, 0xFFFFFFC0ull);
             return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint64_t, NT, STAGE, KR, KX>(
                 keys, offsets, key_len, n, c, words, overwrite, st, chunk, tp);

@@ -50,6 +50,7 @@ enum Knob : int {
                         //                   power-of-two tiles only, else that many tiles
     kKnobBinPipe,       // NB_BIN_PIPE       1: the pipelined bin kernel for 16-byte keys at
                         //                   k = 7 over 385-1 024 tiles (C4); 0: off
+    kKnobBinMix,        // NB_BIN_MIX        1: bin blocks of two sizes (3 / 2 keys per thread)
     kKnobProbePath,     // NB_PROBE_PATH     0 auto | 1 "lane" (one lane per key) | 2 "tiled"
     kKnobFailBuilds,    // NB_FAIL_BUILDS    fault injection: the next N device builds fail
                         //                   with NB_ERR_HIP before launching anything

@@ -66,3 +66,20 @@ def test_bin_pipe_spill_chunks_and_other_m(dev, oracle, knobs):
     buf = synth.fixed_keys(1_200_000, 16, seed=32)
     got = build_into(dev, np.zeros(nbm.nwords(m2), np.uint64), buf, 1_200_000, m2, k, overwrite=False)
     np.testing.assert_array_equal(got, oracle.build(0, buf, None, 16, 1_200_000, m2, k, SEED))
+
+
+@pytest.mark.parametrize("n", [2305, 30_721, 1_500_001])
+def test_bin_mix_c4_shape(dev, oracle, knobs, n):
+    """NB_BIN_MIX: bin blocks of two sizes (2 304 / 1 536 keys; 16-block groups, the
+    last group ragged and partly empty) give the same filter, overwrite and
+    accumulate."""
+    from nasp_bloom import synth
+    import nasp_bloom as nbm
+    knobs(NB_BUILD_PATH="tiled", NB_BIN_MIX="1")
+    m, k = 958_505_838, 7
+    buf = synth.fixed_keys(n + 100_000, 16, seed=33)
+    stale = np.full(nbm.nwords(m), np.uint64(0xFFFFFFFFFFFFFFFF), np.uint64)
+    got = build_into(dev, stale, buf, n, m, k, overwrite=True)
+    np.testing.assert_array_equal(got, oracle.build(0, buf, None, 16, n, m, k, SEED))
+    got2 = build_into(dev, got, buf[16 * n:], 100_000, m, k, overwrite=False)
+    np.testing.assert_array_equal(got2, oracle.build(0, buf, None, 16, n + 100_000, m, k, SEED))
