@@ -2073,6 +2073,7 @@ uint32_t cap_for(uint32_t T, uint32_t G, uint64_t n, uint32_t k);
 bool counted_tiles(uint32_t m, uint64_t n_chunk, uint32_t k, const TileCfg &p2, TileCfg *out) {
     const uint64_t kv = knob(nb::kKnobTileCount);
     if (kv == 1 || m < (1u << 24)) return false;
+    if (kv == 0 && knob(nb::kKnobTileBits)) return false;  // an explicit tile size wins
     constexpr uint64_t kMaxBits = (160 * 1024 - (2 * kShards + 1) * 4) * 8ull - 128;
     const uint64_t tmin = ((uint64_t)m + kMaxBits - 1) / kMaxBits;
     uint64_t T = kv;
@@ -2168,6 +2169,11 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
                    const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st,
                    uint64_t chunk, const TileCfg &tc) {
     constexpr uint64_t kpb = (uint64_t)KPT * NT;
+    // counted tiles (a tile map other than a shift) exist only for the packed
+    // two-tile tail; anything else would find tiles by shifting and scatter out of
+    // range -- refuse it rather than launch it
+    if (tc.mul != pow2_mul(tc.ts) && !(sizeof(ENTRY) == 8 && KR > 0 && tc.T <= 2u * NT))
+        return fail(NB_ERR_ARG, "internal: counted tiles on a path that shifts");
     Workspace *ws;
     TileScratch sc;
     int rc;
@@ -2431,12 +2437,14 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
             if (STAGE) b = std::max<size_t>(b, stage_lds_bytes(NT));
             return b + (size_t)bin_sort_offset_words(T) * 4;
         };
+        // counted tiles only where the packed tail will take them: every other path
+        // finds a tile by shifting (power-of-two tiles)
+        const bool can_pack = tc.ts <= 20 && NB_TWO_TILE && knob(nb::kKnobPack) != 0;
         TileCfg ct;
-        if (tc.ts <= 20 && counted_tiles(c.fm.m, chunk, c.k, tc, &ct) && ct.T <= 2u * NT &&
+        if (can_pack && counted_tiles(c.fm.m, chunk, c.k, tc, &ct) && ct.T <= 2u * NT &&
             pk_lds_of(ct.T) <= 80 * 1024)
             tc = ct;
-        if (tc.ts <= 21 && tc.T <= 2u * NT && NB_TWO_TILE && pk_lds_of(tc.T) <= 80 * 1024 &&
-            knob(nb::kKnobPack) != 0) {
+        if (can_pack && tc.T <= 2u * NT && pk_lds_of(tc.T) <= 80 * 1024) {
             TileCfg tp = tc;
             tp.mix = KPT == 3 && knob(nb::kKnobBinMix) != 0 ? 1u : 0u;
             const uint64_t nblk = tp.mix ? bin_mix_blocks(chunk, kpb, kpb - NT) : (chunk + kpb - 1) / kpb;

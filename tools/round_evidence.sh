@@ -8,7 +8,7 @@ O=gpurun_out/ev_$TAG
 mkdir -p "$O"
 export TMPDIR=/tmp
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { echo smoke failed; exit 1; }
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1
 rc=$?; echo "pytest rc=$rc" >> "$O/pytest_gpu.log"; tail -2 "$O/pytest_gpu.log"
 [ $rc -eq 0 ] || exit 2
 # the driver's default line: C4 (+ C2, probe, host path, 8-core reference baseline)
