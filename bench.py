@@ -328,7 +328,23 @@ def kernel_sha():
     return h.hexdigest()[:16]
 
 
+# The JSON line is the only thing bench.py writes to stdout: everything else written
+# to file descriptor 1 -- e.g. the RCCL banner its communicator prints on init, or
+# library notes -- is sent to stderr, and the line goes to a saved copy of stdout.
+_JSON_OUT = None
+
+
+def emit(obj):
+    out = _JSON_OUT or sys.stdout
+    out.write(json.dumps(obj) + "\n")
+    out.flush()
+
+
 def main():
+    global _JSON_OUT
+    sys.stdout.flush()
+    _JSON_OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -473,7 +489,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(wl, keys_np, offs_np, key_len, args.cpu_budget,
                                            threads=8 if args.workload == "c4" else 1)
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         dist.destroy_process_group()
 
@@ -554,7 +570,7 @@ def bench_merkle(args, world, rank, dev):
         except FileNotFoundError:
             pass
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     if world > 1:
         dist.destroy_process_group()
 
@@ -664,7 +680,7 @@ def bench_cooperative(args, wl, world, rank, dev):
     if world == 1 and not args.no_rank_share:
         res["per_rank_at_8"] = rank_share_rate(nbm, wl, keys, seed, args.flavor, dev, stream)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        emit(res)
     dist.destroy_process_group()
 
 
