@@ -83,7 +83,8 @@ uint64_t nb_device_merkle_count(void);
  * NB_ENTRY32, NB_RANK, NB_FIXED32, NB_FPMOD, NB_KEXACT, NB_BIN_WIDE, NB_OVERLAP (two-level
  * sub-passes pipelined over a second stream of the workspace: 0 off, 1/2 normal/high
  * priority, +4 tile kernels beside the next pass's bin kernel; default 6),
- * NB_SUBPASSES (bin + re-bin sub-passes per tile pass, default 2), NB_FINE_BITS,
+ * NB_SUBPASSES (bin + re-bin sub-passes per tile pass; default 0: 2 for builds of
+ * several passes, 1 for one), NB_FINE_BITS,
  * NB_TILE_COUNT (0 counted-tile policy, 1 power-of-two tiles only, else that many),
  * NB_BIN_PIPE (the pipelined bin kernel for C4's shape), NB_BIN_MIX (bin blocks of two sizes),
  * NB_SHARDED_STAGE, NB_FAIL_BUILDS / NB_FAIL_MERKLES (the next N device builds /

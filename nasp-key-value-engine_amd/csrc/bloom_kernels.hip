@@ -2281,7 +2281,12 @@ int launch_two_level(const uint8_t *keys, const uint64_t *offsets, uint32_t key_
     int rc;
     if ((rc = get_ws(st, &ws))) return rc;
     std::lock_guard<std::mutex> lk(ws->mu);
-    const uint64_t nsub = std::max<uint64_t>(1, std::min<uint64_t>(knob(nb::kKnobSubpasses), 64));
+    // sub-passes: NB_SUBPASSES, or by policy 2 when the build takes several passes (the
+    // C5 step at N = 1: 34.6 -> 33.6 ms pipelined, profiles/r03_ab_c5_subpasses.txt)
+    // and 1 for a single pass (one rank's share at N = 8: 4.38-4.43 vs 4.48-4.51 ms,
+    // profiles/r04_ab_c5r_subpasses.txt)
+    const uint64_t kn = knob(nb::kKnobSubpasses);
+    const uint64_t nsub = kn ? std::min<uint64_t>(kn, 64) : (n > chunk ? 2 : 1);
     const uint64_t sub = std::min<uint64_t>(chunk, ((chunk + nsub - 1) / nsub + kpb - 1) / kpb * kpb);
     const uint64_t spp = (chunk + sub - 1) / sub;  // sub-passes per pass
     // pass-1 capacity in units: the entries' plus <= 4 pad slots per bin block of

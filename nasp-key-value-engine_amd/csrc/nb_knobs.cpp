@@ -24,7 +24,7 @@ constexpr KnobDef kDefs[nb::kKnobCount] = {
     {"NB_PACK5", 1},         {"NB_ENTRY32", 0},     {"NB_RANK", 1},
     {"NB_FIXED32", 1},       {"NB_FPMOD", 1},       {"NB_KEXACT", 1},
     {"NB_BIN_WIDE", 1},      {"NB_SHARDED_STAGE", 0},
-    {"NB_OVERLAP", 6},       {"NB_SUBPASSES", 2},
+    {"NB_OVERLAP", 6},       {"NB_SUBPASSES", 0},
     {"NB_FINE_BITS", 0},     {"NB_TILE_COUNT", 0},
     {"NB_BIN_PIPE", 0},      {"NB_BIN_MIX", 0},
     {"NB_PROBE_PATH", 0},    {"NB_FAIL_BUILDS", 0}, {"NB_FAIL_MERKLES", 0},

@@ -42,7 +42,8 @@ enum Knob : int {
                         //                   priority; + 4: a pass's first bin kernel does
                         //                   not wait for the previous pass's tile kernel;
                         //                   0: no pipelining
-    kKnobSubpasses,     // NB_SUBPASSES      bin + re-bin sub-passes per tile pass (2)
+    kKnobSubpasses,     // NB_SUBPASSES      bin + re-bin sub-passes per tile pass (0: 2 for
+                        //                   multi-pass builds, 1 for a single pass)
     kKnobFineBits,      // NB_FINE_BITS      0: fine-tile policy (2^20 bits); 19: 2^19-bit fine
                         //                   tiles in the two-level build
     kKnobTileCount,     // NB_TILE_COUNT     0: counted-tile policy (single-level packed path:
