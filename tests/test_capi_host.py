@@ -151,3 +151,16 @@ def test_cpu_paths_read_only_key_bytes(built, oracle):
             np.testing.assert_array_equal(w, oracle.build(fl, pad, None, kl, n, m, k, seed))
             np.testing.assert_array_equal(nbm.probe_cpu(keys, None, kl, n, m, k, seed, fl, w),
                                           np.ones(n, np.uint8))
+
+
+def test_round4_knob_defaults(built):
+    """Round 4's switches exist with their product defaults: the counted-tile policy
+    (NB_TILE_COUNT 0), the measured-slower bin variants off (NB_BIN_PIPE, NB_BIN_MIX 0)
+    and the sub-pass policy (NB_SUBPASSES 0: 2 for multi-pass builds, 1 for a single
+    pass) -- unless the environment of this process set them."""
+    import nasp_bloom as nbm
+    for name in ("NB_TILE_COUNT", "NB_BIN_PIPE", "NB_BIN_MIX", "NB_SUBPASSES"):
+        if name not in os.environ:
+            assert nbm.get_knob(name) == 0, name
+    with nbm.knobs(NB_TILE_COUNT=768, NB_BIN_PIPE=1):
+        assert nbm.get_knob("NB_TILE_COUNT") == 768 and nbm.get_knob("NB_BIN_PIPE") == 1
