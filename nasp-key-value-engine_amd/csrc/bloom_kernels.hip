@@ -337,7 +337,16 @@ struct TileCfg {
     uint32_t fmul;   // spill-flag tile of r = __umulhi(r, fmul) (the fts tiling)
     uint32_t w64;    // LDS words (u64) of one tile in the tile kernel, boundary words incl.
     uint32_t mix = 0;  // bin kernel (KPT = 3, packed): blocks of two sizes, see bin_block_keys
+    uint32_t gmajor = 0;  // bucket layout: 0 [T][G][cap], 1 [G][T][cap] (bucket_region)
 };
+
+// First entry (in units of cap) of the bucket of tile t, shard g.  Shard g's runs
+// come from the bin blocks with blockIdx % G == g, which -- blocks go round-robin
+// over the 8 XCDs -- run on one XCD: shard-major buckets ([G][T]) keep each XCD's
+// scattered run writes inside its own 1/G of the bucket array instead of all of it.
+__host__ __device__ inline uint32_t bucket_region(const TileCfg &tc, uint32_t t, uint32_t g) {
+    return tc.gmajor ? g * tc.T + t : t * tc.G + g;
+}
 
 __host__ __device__ inline uint64_t tile_start(uint32_t t, uint32_t mul) {
     return (((uint64_t)t << 32) + mul - 1) / mul;
@@ -654,7 +663,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
             }
             st /= PK;
         }
-        GX[t] = ((t * tc.G + shard) * tc.cap + g - st) * esz;
+        GX[t] = (bucket_region(tc, t, shard) * tc.cap + g - st) * esz;
         return st;
     };
     uint32_t sa = 0, sbb = 0;
@@ -1094,7 +1103,7 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
         int ovf = 0;
         auto run_pair = [&](int u, uint32_t t) {
             const uint32_t st = S[t], g = gres[u];
-            gl_g[u] = (t * tc.G + shard) * tc.cap + g - st;
+            gl_g[u] = bucket_region(tc, t, shard) * tc.cap + g - st;
             gl_l[u] = st + (g < tc.cap ? tc.cap - g : 0u);
             ovf |= (uint64_t)g + hcnt[u] > tc.cap;
         };
@@ -1332,7 +1341,7 @@ __global__ __launch_bounds__(kPipeThreads, 1) void bloom_bin_pipe_kernel(
                 } else {
                     // pathological duplicates: a word past its bucket's capacity goes to
                     // the spill bitmap (its position in the bucket from the run table)
-                    const uint32_t pos = (g + w * 8u) / 8u - (t * tc.G + shard) * tc.cap;
+                    const uint32_t pos = (g + w * 8u) / 8u - bucket_region(tc, t, shard) * tc.cap;
                     if (pos < tc.cap) {
                         bucket_store(reinterpret_cast<uint64_t *>(bb + (g + w * 8u)), word);
                     } else {
@@ -1403,7 +1412,7 @@ __global__ __launch_bounds__(kPipeThreads, 1) void bloom_bin_pipe_kernel(
             reset(p, tid - kPipeH, kPipeThreads - kPipeH);
         }
         if (t < T) {
-            gx_of(q)[t] = ((t * tc.G + shard) * tc.cap + ga - st / 3) * 8u;
+            gx_of(q)[t] = (bucket_region(tc, t, shard) * tc.cap + ga - st / 3) * 8u;
             if ((uint64_t)ga + u > tc.cap) mq[17] = 1u;
         }
         lds_barrier();
@@ -1477,7 +1486,7 @@ __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
     for (uint32_t u = 0; u < UPT; ++u) {
         const uint32_t q = min(first + tid + u * kRebinThreads, first + cntu - 1);
         while (g + 1 < t1.G && q >= v0[g + 1]) ++g;
-        const size_t at = (size_t)(s * t1.G + g) * t1.cap + (q - v0[g]);
+        const size_t at = (size_t)bucket_region(t1, s, g) * t1.cap + (q - v0[g]);
         if constexpr (IN5) p[u] = bucket_load(reinterpret_cast<const uint4 *>(b1v) + at);
         else v[u] = reinterpret_cast<const uint32_t *>(b1v)[at];
     }
@@ -1529,7 +1538,7 @@ __global__ __launch_bounds__(kRebinThreads) void bloom_rebin_kernel(
     }
     if (tid < kSuperFine) {
         const uint32_t t = fbase + tid;
-        fGX[tid] = (t * t2.G + fshard) * t2.cap + gr - fstu;
+        fGX[tid] = bucket_region(t2, t, fshard) * t2.cap + gr - fstu;
         flim[tid] = fstu + (gr < t2.cap ? t2.cap - gr : 0u);
         if ((uint64_t)gr + fu > t2.cap) any_ovf = 1;
     }
@@ -1617,13 +1626,12 @@ __global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
         }
     };
     // the G shards as one flat range of 16-byte vectors
-    const ENTRY *tile_base = buckets + (size_t)t * tc.G * tc.cap;
     const uint32_t nvec = shard_v0[tc.G];
     // a lane's vector indices only grow, so its shard index is advanced, never searched
     uint32_t g = 0;
     auto vec_at = [&](uint32_t v) {
         while (g + 1 < tc.G && v >= shard_v0[g + 1]) ++g;
-        const uint4 *ev = reinterpret_cast<const uint4 *>(tile_base + (size_t)g * tc.cap);
+        const uint4 *ev = reinterpret_cast<const uint4 *>(buckets + (size_t)bucket_region(tc, t, g) * tc.cap);
         return bucket_load(ev + (v - shard_v0[g]));
     };
     uint32_t q = tid;
@@ -1637,7 +1645,7 @@ __global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
     for (; q < nvec; q += NT) or_vec(vec_at(q));
     if (tid < tc.G) {  // each shard's tail (< kPerVec entries)
         const uint32_t cnt = shard_cnt[tid];
-        const ENTRY *e = tile_base + (size_t)tid * tc.cap;
+        const ENTRY *e = buckets + (size_t)bucket_region(tc, t, tid) * tc.cap;
         for (uint32_t r = cnt / kPerVec * kPerVec; r < cnt; ++r) {
             const uint64_t x = (uint64_t)e[r];
             orv((uint32_t)x);
@@ -1732,7 +1740,7 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
     uint32_t *cur = sc.gcur + (size_t)shard * T;
     for (uint32_t t = tid; t < T; t += NT) {
         const uint32_t h = cnt[t], g = h ? atomicAdd(&cur[t], h) : 0u;
-        GX[t] = (t * tc.G + shard) * tc.cap + g - S[t];
+        GX[t] = bucket_region(tc, t, shard) * tc.cap + g - S[t];
         L[t] = S[t] + (g < tc.cap ? tc.cap - g : 0u);
     }
     // placement (the reservations' round trips overlap it)
@@ -1791,7 +1799,6 @@ __global__ __launch_bounds__(NT) void probe_tile_kernel(TileCfg tc, TileScratch 
         shard_v0[tc.G] = v0;
     }
     __syncthreads();
-    const uint64_t *tb = buckets + (size_t)t * tc.G * tc.cap;
     const uint32_t ne = shard_v0[tc.G];
     auto test = [&](uint64_t e) {
         const uint32_t off = (uint32_t)e & mask;
@@ -1802,7 +1809,7 @@ __global__ __launch_bounds__(NT) void probe_tile_kernel(TileCfg tc, TileScratch 
     uint32_t g = 0;
     auto entry_at = [&](uint32_t q) {
         while (g + 1 < tc.G && q >= shard_v0[g + 1]) ++g;
-        return tb[(size_t)g * tc.cap + (q - shard_v0[g])];
+        return buckets[(size_t)bucket_region(tc, t, g) * tc.cap + (q - shard_v0[g])];
     };
     uint32_t q = tid;
     for (; q + 3 * NT < ne; q += 4 * NT) {
@@ -2018,6 +2025,7 @@ using nb::knob;  // the A/B switches (nb_knobs.h): read once, atomics
 // C5: ts = 20, 4 096 fine tiles.
 TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     TileCfg tc;
+    tc.gmajor = knob(nb::kKnobBucketGMajor) != 0;
     uint32_t ts = 12;
     while (ts < 16 && ((uint64_t)m >> (ts + 1)) >= 1024) ++ts;
     while (ts < 20 && (((uint64_t)m + (1ull << ts) - 1) >> ts) > 2048) ++ts;
@@ -2571,6 +2579,7 @@ int launch_build_f(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
 // leaves >= 256 tiles; cap per (tile, shard) as the build's.
 TileCfg probe_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     TileCfg tc;
+    tc.gmajor = knob(nb::kKnobBucketGMajor) != 0;
     uint32_t ts = 12;
     while (ts < 20 && (((uint64_t)m + (1ull << (ts + 1)) - 1) >> (ts + 1)) >= 256) ++ts;
     tc.ts = ts;
@@ -2625,7 +2634,9 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
     if ((rc = get_ws(st, &ws))) return rc;
     std::lock_guard<std::mutex> lk(ws->mu);
     // chunks whose 64-bit entries stay under ~6 GB of buckets (key ids < 2^32)
-    const uint64_t budget = std::max<uint64_t>(NT, (6ull << 30) / (10ull * c.k));
+    const uint64_t kc = knob(nb::kKnobProbeChunk);
+    const uint64_t budget = std::max<uint64_t>(NT, kc ? std::min<uint64_t>(kc, (6ull << 30) / (10ull * c.k))
+                                                      : (6ull << 30) / (10ull * c.k));
     const uint64_t passes = (n + budget - 1) / budget;
     const uint64_t chunk = std::max<uint64_t>(1, (n + passes - 1) / passes);
     const TileCfg tc = probe_tiles(c.fm.m, chunk, c.k);

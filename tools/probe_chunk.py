@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Tiled batch probe by key-range passes (NB_PROBE_CHUNK), same box, interleaved.
+
+A miss in the tiled probe is a byte store into the key's answer (≈ k/2 per absent
+key).  Over 100M keys those stores land anywhere in a 100 MB answer
+array; split into passes of C keys, a pass's stores stay inside C bytes, which the
+XCDs' 4 MiB L2s can hold -- at the price of one read of the filter per pass.  This
+times the tiled path at several C against the lane path on C4's filter, for present,
+absent and half-present batches, and checks every answer against the lane path's.
+
+  python tools/probe_chunk.py [--reps R] [--chunks 0,25000000,...] [--batches present,absent,mixed]
+                               [--no-lane]
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "nasp-key-value-engine_amd"))
+
+
+def main():
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--chunks", default="0,25000000,12500000,6250000,3125000")
+    ap.add_argument("--batches", default="present,absent,mixed")
+    ap.add_argument("--no-lane", action="store_true")
+    args = ap.parse_args()
+    reps = args.reps
+    wl = synth.C4
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.Stream(device=dev)
+    p_np, _, kl = synth.keys_for(wl)
+    a_np, _, _ = synth.keys_for(wl, seed=synth.SEED + 1000)
+    # (the generator's buffers keep their tail padding: kernels may read past a key)
+    present = torch.from_numpy(p_np).to(dev)
+    absent = torch.from_numpy(a_np).to(dev)
+    mixed = present.clone()
+    mv = mixed[:wl.n * kl].view(wl.n, kl)
+    mv[1::2] = absent[:wl.n * kl].view(wl.n, kl)[1::2]
+    batches = {"present": present, "absent": absent, "mixed": mixed}
+    batches = {b: batches[b] for b in args.batches.split(",")}
+    words = torch.zeros(nbm.nwords(wl.m), dtype=torch.int64, device=dev)
+    nbm.build_device(batches["present"], None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, stream=st,
+                     overwrite=True)
+    torch.cuda.synchronize(dev)
+    out = torch.empty(wl.n, dtype=torch.uint8, device=dev)
+    ref = {}
+    with nbm.knobs(NB_PROBE_PATH="lane"):
+        for name, b in batches.items():
+            nbm.probe_device(b, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out, stream=st)
+            torch.cuda.synchronize(dev)
+            ref[name] = out.clone()
+    variants = ([] if args.no_lane else [("lane", "lane", 0)]) + [
+        (f"tiled C={c / 1e6 if c else 'policy'}M", "tiled", c) for c in map(int, args.chunks.split(","))]
+    table = {}
+    bad = 0
+    for rep in range(reps):
+        for label, path, chunk in variants:
+            with nbm.knobs(NB_PROBE_PATH=path, NB_PROBE_CHUNK=str(chunk)):
+                for name, b in batches.items():
+                    nbm.probe_device(b, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out, stream=st)
+                    torch.cuda.synchronize(dev)
+                    if not torch.equal(out, ref[name]):
+                        bad += 1
+                        print(f"MISMATCH {label} {name}", flush=True)
+                    t0 = time.perf_counter()
+                    for _ in range(5):
+                        nbm.probe_device(b, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out,
+                                         stream=st)
+                    torch.cuda.synchronize(dev)
+                    ms = (time.perf_counter() - t0) * 1e3 / 5
+                    table.setdefault((label, name), []).append(ms)
+                    print(f"rep {rep} {label:>16} {name:>8} {ms:8.3f} ms  {wl.n / ms / 1e6:7.2f} Gkeys/s",
+                          flush=True)
+    print("summary (ms per 100M-key call, wall clock over 5 calls; min over reps):")
+    for label, _, _ in variants:
+        print(f"  {label:>16} " + "  ".join(f"{n} {min(table[(label, n)]):7.3f}" for n in batches))
+    print(f"answers identical to the lane path: {'yes' if bad == 0 else f'NO ({bad} mismatches)'}")
+    return 1 if bad else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
