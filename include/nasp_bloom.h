@@ -80,7 +80,7 @@ uint64_t nb_device_merkle_count(void);
  * it for the whole process afterwards (thread-safe).  Names: NB_BUILD_PATH
  * (0 auto, 1 atomic, 2 tiled), NB_PROBE_PATH (0 auto, 1 one lane per key, 2 tiled),
  * NB_PROBE_CHUNK (keys per tiled-probe pass; 0: the policy), NB_BUCKET_GMAJOR (bucket
- * layout: 1 shard-major),
+ * layout: 1 shard-major, the default; 0 tile-major),
  * NB_PACK, NB_TILE_BITS, NB_SHARDS, NB_CHUNK_KEYS, NB_TWO_LEVEL, NB_PACK5,
  * NB_ENTRY32, NB_RANK, NB_FIXED32, NB_FPMOD, NB_KEXACT, NB_BIN_WIDE, NB_OVERLAP (two-level
  * sub-passes pipelined over a second stream of the workspace: 0 off, 1/2 normal/high

@@ -52,7 +52,9 @@ enum Knob : int {
     kKnobBinPipe,       // NB_BIN_PIPE       1: the pipelined bin kernel for 16-byte keys at
                         //                   k = 7 over 385-1 024 tiles (C4); 0: off
     kKnobBinMix,        // NB_BIN_MIX        1: bin blocks of two sizes (3 / 2 keys per thread)
-    kKnobBucketGMajor,  // NB_BUCKET_GMAJOR  1: buckets laid out shard-major ([G][T]), 0: [T][G]
+    kKnobBucketGMajor,  // NB_BUCKET_GMAJOR  1 (default): buckets laid out shard-major
+                        //                   ([G][T][cap]: one XCD's runs in 1/G of them),
+                        //                   0: tile-major ([T][G][cap])
     kKnobProbePath,     // NB_PROBE_PATH     0 auto | 1 "lane" (one lane per key) | 2 "tiled"
     kKnobProbeChunk,    // NB_PROBE_CHUNK    0: tiled-probe pass policy, else keys per pass
     kKnobFailBuilds,    // NB_FAIL_BUILDS    fault injection: the next N device builds fail

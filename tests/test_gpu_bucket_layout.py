@@ -1,6 +1,6 @@
-"""GPU parity of the shard-major bucket layout (round 4, bloom_kernels.hip
-bucket_region, NB_BUCKET_GMAJOR=1): the same entries in [G][T] instead of [T][G]
-order, on every path that writes or reads buckets -- the single-level bin kernel
+"""GPU parity of both bucket layouts (round 4, bloom_kernels.hip bucket_region):
+shard-major [G][T] (NB_BUCKET_GMAJOR=1, the default) and tile-major [T][G] (0), on
+every path that writes or reads buckets -- the single-level bin kernel
 (packed 21-bit and 32-bit entries, counted and power-of-two tiles, spill), the
 two-level build (pass-1 Pack5 units, re-bin, fine tiles), the pipelined bin kernel and
 the tiled probe in several key-range passes (NB_PROBE_CHUNK).  Bit-exact against the
@@ -42,12 +42,13 @@ CASES = [
 ]
 
 
+@pytest.mark.parametrize("gmajor", ["0", "1"])
 @pytest.mark.parametrize("case", range(len(CASES)))
-def test_gmajor_build(dev, oracle, knobs, case):
+def test_gmajor_build(dev, oracle, knobs, case, gmajor):
     from nasp_bloom import synth
     import nasp_bloom as nbm
     m, k, kl, extra = CASES[case]
-    knobs(NB_BUILD_PATH="tiled", NB_BUCKET_GMAJOR="1", **extra)
+    knobs(NB_BUILD_PATH="tiled", NB_BUCKET_GMAJOR=gmajor, **extra)
     n = 300_000
     buf = synth.fixed_keys(2 * n, kl, seed=31)
     stale = np.full(nbm.nwords(m), np.uint64(0xFFFFFFFFFFFFFFFF), np.uint64)
@@ -60,13 +61,14 @@ def test_gmajor_build(dev, oracle, knobs, case):
     np.testing.assert_array_equal(got, oracle.build(1, vbuf, voffs, 0, n, m, k, SEED))
 
 
+@pytest.mark.parametrize("gmajor", ["0", "1"])
 @pytest.mark.parametrize("m,k,kl", [(958_505_838, 7, 16), (2**32 - 1, 10, 32)])
-def test_gmajor_spill(dev, oracle, knobs, m, k, kl):
-    """Duplicated keys past the buckets' capacity (spill bitmap) in the shard-major
-    layout, then a normal build is exact again (cursors and spill scratch clean)."""
+def test_gmajor_spill(dev, oracle, knobs, m, k, kl, gmajor):
+    """Duplicated keys past the buckets' capacity (spill bitmap) in either layout,
+    then a normal build is exact again (cursors and spill scratch clean)."""
     from nasp_bloom import synth
     import nasp_bloom as nbm
-    knobs(NB_BUILD_PATH="tiled", NB_BUCKET_GMAJOR="1", NB_CHUNK_KEYS="70000")
+    knobs(NB_BUILD_PATH="tiled", NB_BUCKET_GMAJOR=gmajor, NB_CHUNK_KEYS="70000")
     stale = np.full(nbm.nwords(m), np.uint64(0xFFFFFFFFFFFFFFFF), np.uint64)
     n = 300_000
     dup = np.zeros(n * kl + 16, np.uint8)
@@ -81,7 +83,7 @@ def test_gmajor_spill(dev, oracle, knobs, m, k, kl):
 @pytest.mark.parametrize("gmajor", ["0", "1"])
 @pytest.mark.parametrize("chunk", ["0", "1000000"])
 def test_gmajor_tiled_probe(dev, oracle, knobs, gmajor, chunk):
-    """The tiled probe in the shard-major layout and in key-range passes: a filter of
+    """The tiled probe in either layout and in key-range passes: a filter of
     60 % of 4.5M keys probed over all of them, bit-exact."""
     import torch
     import nasp_bloom as nbm
