@@ -11,7 +11,9 @@
 //   4. a chunked pipeline: bin kernels on (256 - x) CUs beside tile kernels on x
 //      CUs, checked bit for bit against the one-shot build.
 //   5. power-of-two (915) vs counted (768) tiles, one-shot builds interleaved.
-// usage: ubench_c4 [all|stops|tiles|mask|pipe]
+//   6. cstops / layout: phase stops in the product configuration (counted tiles,
+//      shard-major buckets), and tile-major vs shard-major buckets interleaved.
+// usage: ubench_c4 [all|stops|cstops|layout|tiles|mask|pipe]
 #include <hip/hip_runtime.h>
 __constant__ int g_diag_stop;
 #define NB_DIAG_STOP(phase) (g_diag_stop == (phase) || ((phase) == 1 && g_diag_stop == 11))
@@ -254,6 +256,103 @@ int main(int argc, char **argv) {
                 if (r >= 1) sum += t;
             }
             printf("tile kernel unroll %2d: best %.4f  mean(5) %.4f ms\n", unroll, best, sum / 5);
+        }
+    }
+
+    if (all || !strcmp(what, "cstops") || !strcmp(what, "layout")) {
+        // the product's configuration: counted tiles (768), shard-major buckets unless
+        // NB_BUCKET_GMAJOR=0.  cstops: phase stops of the bin kernel and the tile
+        // kernel alone; layout: tile-major vs shard-major buckets, interleaved
+        TileCfg p2 = choose_tiles(kM, kN, kK), ct;
+        if (!counted_tiles(kM, kN, kK, p2, &ct)) { printf("counted tiles: policy declined\n"); return 1; }
+        {
+            const uint64_t nblk = (kN + kKPB - 1) / kKPB, bps = (nblk + ct.G - 1) / ct.G;
+            const uint64_t capw = ((uint64_t)ct.cap + 2 * bps + 2) / 3;
+            ct.cap = (uint32_t)((capw + 7) & ~7ull);
+        }
+        CK(hipFuncSetAttribute(reinterpret_cast<const void *>(BIN), hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)std::max(bin_lds_of(tfull), bin_lds_of(ct))));
+        CK(hipFuncSetAttribute(reinterpret_cast<const void *>(bloom_tile_or_kernel<uint64_t, true, kTileThreads, 4>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(ct.w64 * 8 + (2 * kShards + 1) * 4)));
+        TileScratch sc = s.sc[0];
+        sc.zero_words = s.words;
+        auto bin = [&](const TileCfg &tc) {
+            hipLaunchKernelGGL(BIN, dim3((uint32_t)((kN + kKPB - 1) / kKPB)), dim3(kNT), bin_lds_of(tc), s0,
+                               s.keys, nullptr, 16u, kN, s.c, tc, sc, s.bk[0]);
+        };
+        auto tile = [&](const TileCfg &tc) {
+            hipLaunchKernelGGL((bloom_tile_or_kernel<uint64_t, true, kTileThreads, 4>), dim3(tc.T),
+                               dim3(kTileThreads), (size_t)tc.w64 * 8 + (2 * kShards + 1) * 4, s0, tc, s.sc[0],
+                               s.bk[0], s.words, nwords);
+        };
+        printf("product config: counted T=%u, %s buckets\n", ct.T, ct.gmajor ? "shard-major" : "tile-major");
+        for (int r = 0; r < 20; ++r) {  // settle the clock
+            bin(ct);
+            tile(ct);
+        }
+        CK(hipStreamSynchronize(s0));
+        if (!strcmp(what, "cstops") || all) {
+            const char *names[] = {"hash+indices (stop 11)", "+count atomics (stop 1)", "+scan/reserve (stop 2)",
+                                   "+placement (stop 3)", "full bin kernel (stop 0)"};
+            const int stops[] = {11, 1, 2, 3, 0};
+            for (int i = 0; i < 5; ++i) {
+                set_stop(stops[i]);
+                float best = 1e30f, sum = 0;
+                for (int r = 0; r < 7; ++r) {
+                    CK(hipMemsetAsync(s.sc[0].gcur, 0, kCurWords * 4, s0));
+                    Ev e;
+                    CK(hipEventRecord(e.a, s0));
+                    bin(ct);
+                    CK(hipEventRecord(e.b, s0));
+                    const float t = e.ms();
+                    best = std::min(best, t);
+                    if (r >= 2) sum += t;
+                }
+                printf("phase stop %-26s best %.4f  mean(5) %.4f ms\n", names[i], best, sum / 5);
+            }
+            set_stop(0);
+            CK(hipMemsetAsync(s.sc[0].gcur, 0, kCurWords * 4, s0));
+            float best = 1e30f, sum = 0;
+            for (int r = 0; r < 6; ++r) {
+                bin(ct);
+                Ev e;
+                CK(hipEventRecord(e.a, s0));
+                tile(ct);
+                CK(hipEventRecord(e.b, s0));
+                const float t = e.ms();
+                best = std::min(best, t);
+                if (r >= 1) sum += t;
+            }
+            printf("tile kernel: best %.4f  mean(5) %.4f ms\n", best, sum / 5);
+        }
+        if (!strcmp(what, "layout") || all) {
+            float bb[2] = {1e30f, 1e30f}, tt[2] = {1e30f, 1e30f}, sum[2] = {0, 0};
+            for (int r = 0; r < 10; ++r)
+                for (int v = 0; v < 2; ++v) {
+                    TileCfg tc = ct;
+                    tc.gmajor = (uint32_t)v;
+                    CK(hipMemsetAsync(s.words, 0xA5, nwords * 8, s0));
+                    Ev e, f;
+                    CK(hipEventRecord(e.a, s0));
+                    bin(tc);
+                    CK(hipEventRecord(e.b, s0));
+                    CK(hipEventRecord(f.a, s0));
+                    tile(tc);
+                    CK(hipEventRecord(f.b, s0));
+                    const float b = e.ms(), t = f.ms();
+                    bb[v] = std::min(bb[v], b);
+                    tt[v] = std::min(tt[v], t);
+                    if (r >= 2) sum[v] += b + t;
+                    if (r == 9) {
+                        std::vector<uint64_t> a(nwords), ref(nwords);
+                        CK(hipMemcpy(a.data(), s.words, nwords * 8, hipMemcpyDeviceToHost));
+                        CK(hipMemcpy(ref.data(), s.words_ref, nwords * 8, hipMemcpyDeviceToHost));
+                        printf("%s buckets: %s\n", v ? "shard-major" : "tile-major", a == ref ? "bit-exact" : "MISMATCH");
+                    }
+                }
+            for (int v = 0; v < 2; ++v)
+                printf("%s buckets: bin best %.4f, tile best %.4f, build mean(8) %.4f ms\n",
+                       v ? "shard-major" : "tile-major", bb[v], tt[v], sum[v] / 8);
         }
     }
 
