@@ -143,7 +143,8 @@ static int c5_pmc() {
 
 int main(int argc, char **argv) {
     // argv[1]: c2 (default), c4 (the 100M-key shard) or c3 (100M keys of 8-64 bytes);
-    // c5 (pmc only): C5's pass-1 bin kernel; argv[2] == "intmod": integer remainders
+    // c5 (pmc only): C5's pass-1 bin kernel; argv[2] == "intmod": integer remainders;
+    // "c3 product": C3's phase stops in the product configuration
     if (argc > 1 && !strcmp(argv[1], "c5")) return c5_pmc();
     const bool c4 = argc > 1 && !strcmp(argv[1], "c4"), c3 = argc > 1 && !strcmp(argv[1], "c3");
     const uint64_t n = (c4 || c3) ? 100000000 : 10000000;
@@ -202,6 +203,79 @@ int main(int argc, char **argv) {
         }
         set_stop(0);
         printf("pmc dispatches: stops 11 1 2 3 0\n");
+        return 0;
+    }
+    if (c3 && argc > 2 && !strcmp(argv[2], "product")) {
+        // C3 in the product's configuration (launch_tiled: counted tiles, k = 7
+        // exact, shard-major buckets unless NB_BUCKET_GMAJOR=0): phase stops of the
+        // staged bin kernel after a settle, then the tile kernel
+        TileCfg p2 = choose_tiles(m, n, k), ct;
+        if (!counted_tiles(m, n, k, p2, &ct)) ct = p2;
+        constexpr int NT = kBinThreads, KPT = kBinKPT;
+        constexpr uint64_t kpb = (uint64_t)KPT * NT;
+        {
+            const uint64_t nblk = (n + kpb - 1) / kpb, bps = (nblk + ct.G - 1) / ct.G;
+            const uint64_t capw = ((uint64_t)ct.cap + 2 * bps + 2) / 3;
+            ct.cap = (uint32_t)((capw + 7) & ~7ull);
+        }
+        TileScratch scz = sc;
+        scz.zero_words = words;
+        const size_t sort = std::max<size_t>(kpb * c.k * 4 + (size_t)ct.T * 8, stage_lds_bytes(NT));
+        const size_t lds = (size_t)bin_sort_offset_words(ct.T) * 4 + sort;
+        auto kern = bloom_bin_kernel<0, kOffsets, KPT, uint64_t, NT, true, 7, 7>;
+        allow_lds(kern, lds);
+        auto tile = bloom_tile_or_kernel<uint64_t, true>;
+        const size_t tlds = (size_t)ct.w64 * 8 + (2 * kShards + 1) * 4;
+        allow_lds(tile, tlds);
+        printf("C3 product: T=%u mul=%u cap=%u words, %s buckets, bin LDS %zu B\n", ct.T, ct.mul, ct.cap,
+               ct.gmajor ? "shard-major" : "tile-major", lds);
+        auto bin = [&]() {
+            hipLaunchKernelGGL(kern, dim3((uint32_t)((n + kpb - 1) / kpb)), dim3(NT), lds, 0, keys, g_offsets, 0u,
+                               n, c, ct, scz, (uint64_t *)buckets);
+        };
+        auto tl = [&]() {
+            hipLaunchKernelGGL(tile, dim3(ct.T), dim3(kTileThreads), tlds, 0, ct, sc, (const uint64_t *)buckets,
+                               words, ((uint64_t)m + 63) / 64);
+        };
+        for (int r = 0; r < 20; ++r) {  // settle the clock
+            bin();
+            tl();
+        }
+        CK(hipDeviceSynchronize());
+        const char *names[] = {"stage+hash+indices (stop 11)", "+count atomics (stop 1)", "+scan/reserve (stop 2)",
+                               "+placement (stop 3)", "full bin kernel (stop 0)"};
+        const int stops[] = {11, 1, 2, 3, 0};
+        Ev ev;
+        for (int i = 0; i < 5; ++i) {
+            set_stop(stops[i]);
+            float best = 1e30f, sum = 0;
+            for (int r = 0; r < 7; ++r) {
+                CK(hipMemset(sc.gcur, 0, kCurWords * 4));
+                CK(hipEventRecord(ev.a));
+                bin();
+                CK(hipEventRecord(ev.b));
+                CK(hipEventSynchronize(ev.b));
+                float ms;
+                CK(hipEventElapsedTime(&ms, ev.a, ev.b));
+                best = std::min(best, ms);
+                if (r >= 2) sum += ms;
+            }
+            printf("phase stop %-30s best %.4f  mean(5) %.4f ms\n", names[i], best, sum / 5);
+        }
+        set_stop(0);
+        CK(hipMemset(sc.gcur, 0, kCurWords * 4));
+        float best = 1e30f;
+        for (int r = 0; r < 6; ++r) {
+            bin();
+            CK(hipEventRecord(ev.a));
+            tl();
+            CK(hipEventRecord(ev.b));
+            CK(hipEventSynchronize(ev.b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, ev.a, ev.b));
+            best = std::min(best, ms);
+        }
+        printf("tile kernel: best %.4f ms\n", best);
         return 0;
     }
     printf("%s packed: ts=%u T=%u G=%u cap=%u words\n", c3 ? "C3" : c4 ? "C4" : "C2", tc.ts, tc.T, tc.G, tc.cap);
