@@ -79,7 +79,8 @@ uint64_t nb_device_merkle_count(void);
  * environment variable of the same name once, on first use; nb_set_knob changes
  * it for the whole process afterwards (thread-safe).  Names: NB_BUILD_PATH
  * (0 auto, 1 atomic, 2 tiled), NB_PROBE_PATH (0 auto, 1 one lane per key, 2 tiled),
- * NB_PROBE_CHUNK (keys per tiled-probe pass; 0: the policy), NB_BUCKET_GMAJOR (bucket
+ * NB_PROBE_CHUNK (keys per tiled-probe pass; 0: the policy), NB_PROBE_TILED_PCT (auto's
+ * tiled path from this percentage of present keys in its sample, default 30), NB_BUCKET_GMAJOR (bucket
  * layout: 1 shard-major, the default; 0 tile-major),
  * NB_PACK, NB_TILE_BITS, NB_SHARDS, NB_CHUNK_KEYS, NB_TWO_LEVEL, NB_PACK5,
  * NB_ENTRY32, NB_RANK, NB_FIXED32, NB_FPMOD, NB_KEXACT, NB_BIN_WIDE, NB_OVERLAP (two-level
@@ -222,7 +223,7 @@ int nb_build_device_ex(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_
  * path (lookups binned by filter tile and tested in LDS: ~4x the one-lane-per-key
  * rate for present keys, ~half of it for absent ones); NB_PROBE_PATH=0 (auto)
  * probes the first 4 096 keys one lane per key and picks the tiled path when at
- * least half of them were present.  Auto waits once for that sample (its 16 counts
+ * least 30 % of them were present (NB_PROBE_TILED_PCT).  Auto waits once for that sample (its 16 counts
  * land in host-mapped memory) -- except while the stream is being captured into a graph,
  * where both paths are launched and gated on the sample on the device.  Same
  * answers on every path. */

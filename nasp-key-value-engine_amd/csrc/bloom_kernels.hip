@@ -255,13 +255,20 @@ struct ProbeGate {
     uint32_t blocks;         // sample blocks (words of decide)
     uint32_t sample;         // keys in the sample
     uint32_t want;           // 1 the lane path, 2 the tiled path
+    uint32_t pct = 30;       // tiled from this percentage of the sample present on
 };
+// Auto's choice from the sample's hit count h of s keys: tiled when at least pct %
+// were present (a present key costs the lane kernel ~k gathers, an
+// absent one ~2, and the tiled path a fixed pass plus ~k/2 stores per absent key;
+// on C3 / C4's filter the two break even at 28-30 % present)
+__host__ __device__ inline bool probe_pick_tiled(uint64_t h, uint64_t s, uint32_t pct) {
+    return 100 * h >= (uint64_t)pct * s;
+}
 __device__ __forceinline__ bool gate_open(const ProbeGate &g) {
     if (!g.decide) return true;
     uint32_t h = 0;  // uniform: scalar loads
     for (uint32_t b = 0; b < g.blocks; ++b) h += g.decide[b];
-    // tiled when at least half the sample was present
-    const uint32_t choice = 2ull * h >= g.sample ? 2u : 1u;
+    const uint32_t choice = probe_pick_tiled(h, g.sample, g.pct) ? 2u : 1u;
     return choice == g.want;
 }
 
@@ -2677,6 +2684,7 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     const bool tiled_ok = kTiledLayout && c.k <= kmax && pT <= kMaxTiles &&
                           probe_bin_lds_bytes(pT, c.k, !vec_layout(LAYOUT)) <= kMaxBlockLds;
     const ProbeGate none{nullptr, nullptr, 0, 0, 0};
+    const uint32_t pct = (uint32_t)std::min<uint64_t>(knob(nb::kKnobProbeTiledPct), 101);
     if (path == 1 || !tiled_ok || (path == 0 && n < kProbeTiledMin))
         return launch_probe_lane<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, out, st, none);
     auto tiled = [&](const uint8_t *k_, const uint64_t *o_, uint64_t n_, uint8_t *out_,
@@ -2728,11 +2736,11 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         volatile uint32_t *hs = ws->probe_hits_host;
         uint64_t h = 0;
         for (uint32_t b = 0; b < kProbeSampleBlocks; ++b) h += hs[b];
-        if (2 * h >= S) return tiled(rk, ro, n - S, out + S, none);  // as gate_open decides
+        if (probe_pick_tiled(h, S, pct)) return tiled(rk, ro, n - S, out + S, none);  // as gate_open decides
         return launch_probe_lane<FLAVOR, LAYOUT>(rk, ro, key_len, n - S, c, words, out + S, st, none);
     }
-    const ProbeGate lane{nullptr, ws->probe_hits, kProbeSampleBlocks, (uint32_t)S, 1};
-    const ProbeGate tile{nullptr, ws->probe_hits, kProbeSampleBlocks, (uint32_t)S, 2};
+    const ProbeGate lane{nullptr, ws->probe_hits, kProbeSampleBlocks, (uint32_t)S, 1, pct};
+    const ProbeGate tile{nullptr, ws->probe_hits, kProbeSampleBlocks, (uint32_t)S, 2, pct};
     if ((rc = launch_probe_lane<FLAVOR, LAYOUT>(rk, ro, key_len, n - S, c, words, out + S, st, lane)))
         return rc;
     return tiled(rk, ro, n - S, out + S, tile);

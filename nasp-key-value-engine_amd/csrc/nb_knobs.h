@@ -57,6 +57,8 @@ enum Knob : int {
                         //                   0: tile-major ([T][G][cap])
     kKnobProbePath,     // NB_PROBE_PATH     0 auto | 1 "lane" (one lane per key) | 2 "tiled"
     kKnobProbeChunk,    // NB_PROBE_CHUNK    0: tiled-probe pass policy, else keys per pass
+    kKnobProbeTiledPct, // NB_PROBE_TILED_PCT auto: the tiled path from this % of the sample
+                        //                   present (default 30; 50 before round 4's end)
     kKnobFailBuilds,    // NB_FAIL_BUILDS    fault injection: the next N device builds fail
                         //                   with NB_ERR_HIP before launching anything
     kKnobFailMerkles,   // NB_FAIL_MERKLES   the same for device Merkle trees

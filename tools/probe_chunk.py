@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--chunks", default="0,25000000,12500000,6250000,3125000")
     ap.add_argument("--batches", default="present,absent,mixed")
     ap.add_argument("--no-lane", action="store_true")
+    ap.add_argument("--auto-pct", default="", help="auto path at these NB_PROBE_TILED_PCT values")
     args = ap.parse_args()
     reps = args.reps
     wl = synth.C4
@@ -45,9 +46,14 @@ def main():
     mv = mixed[:wl.n * kl].view(wl.n, kl)
     mv[1::2] = absent[:wl.n * kl].view(wl.n, kl)[1::2]
     batches = {"present": present, "absent": absent, "mixed": mixed}
+    for pc in (20, 30, 40):  # pc % present: keys i with i % 10 < pc / 10 (the sample sees the same mix)
+        b = absent.clone()
+        bv, pv = b[:wl.n * kl].view(wl.n // 10, 10, kl), present[:wl.n * kl].view(wl.n // 10, 10, kl)
+        bv[:, :pc // 10] = pv[:, :pc // 10]
+        batches[f"p{pc}"] = b
     batches = {b: batches[b] for b in args.batches.split(",")}
     words = torch.zeros(nbm.nwords(wl.m), dtype=torch.int64, device=dev)
-    nbm.build_device(batches["present"], None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, stream=st,
+    nbm.build_device(present, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, stream=st,
                      overwrite=True)
     torch.cuda.synchronize(dev)
     out = torch.empty(wl.n, dtype=torch.uint8, device=dev)
@@ -57,13 +63,14 @@ def main():
             nbm.probe_device(b, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out, stream=st)
             torch.cuda.synchronize(dev)
             ref[name] = out.clone()
-    variants = ([] if args.no_lane else [("lane", "lane", 0)]) + [
-        (f"tiled C={c / 1e6 if c else 'policy'}M", "tiled", c) for c in map(int, args.chunks.split(","))]
+    variants = ([] if args.no_lane else [("lane", "lane", 0, "30")]) + [
+        (f"tiled C={c / 1e6 if c else 'policy'}M", "tiled", c, "30") for c in map(int, args.chunks.split(",") if args.chunks else [])
+    ] + [(f"auto pct={p}", "auto", 0, p) for p in filter(None, args.auto_pct.split(","))]
     table = {}
     bad = 0
     for rep in range(reps):
-        for label, path, chunk in variants:
-            with nbm.knobs(NB_PROBE_PATH=path, NB_PROBE_CHUNK=str(chunk)):
+        for label, path, chunk, pct in variants:
+            with nbm.knobs(NB_PROBE_PATH=path, NB_PROBE_CHUNK=str(chunk), NB_PROBE_TILED_PCT=pct):
                 for name, b in batches.items():
                     nbm.probe_device(b, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out, stream=st)
                     torch.cuda.synchronize(dev)
@@ -80,7 +87,7 @@ def main():
                     print(f"rep {rep} {label:>16} {name:>8} {ms:8.3f} ms  {wl.n / ms / 1e6:7.2f} Gkeys/s",
                           flush=True)
     print("summary (ms per 100M-key call, wall clock over 5 calls; min over reps):")
-    for label, _, _ in variants:
+    for label, _, _, _ in variants:
         print(f"  {label:>16} " + "  ".join(f"{n} {min(table[(label, n)]):7.3f}" for n in batches))
     print(f"answers identical to the lane path: {'yes' if bad == 0 else f'NO ({bad} mismatches)'}")
     return 1 if bad else 0
