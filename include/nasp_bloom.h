@@ -80,18 +80,17 @@ uint64_t nb_device_merkle_count(void);
  * it for the whole process afterwards (thread-safe).  Names: NB_BUILD_PATH
  * (0 auto, 1 atomic, 2 tiled), NB_PROBE_PATH (0 auto, 1 one lane per key, 2 tiled),
  * NB_PROBE_CHUNK (keys per tiled-probe pass; 0: the policy), NB_PROBE_TILED_PCT (auto's
- * tiled path from this percentage of present keys in its sample, default 30), NB_BUCKET_GMAJOR (bucket
- * layout: 1 shard-major, the default; 0 tile-major),
+ * tiled path from this percentage of present keys in its sample, default 30),
  * NB_PACK, NB_TILE_BITS, NB_SHARDS, NB_CHUNK_KEYS, NB_TWO_LEVEL, NB_PACK5,
  * NB_ENTRY32, NB_RANK, NB_FIXED32, NB_FPMOD, NB_KEXACT, NB_BIN_WIDE, NB_OVERLAP (two-level
  * sub-passes pipelined over a second stream of the workspace: 0 off, 1/2 normal/high
  * priority, +4 tile kernels beside the next pass's bin kernel; default 6),
  * NB_SUBPASSES (bin + re-bin sub-passes per tile pass; default 0: 2 for builds of
- * several passes, 1 for one), NB_FINE_BITS,
+ * several passes, 1 for one -- 0 is the policy, not one sub-pass),
  * NB_TILE_COUNT (0 counted-tile policy, 1 power-of-two tiles only, else that many),
- * NB_BIN_PIPE (the pipelined bin kernel for C4's shape), NB_BIN_MIX (bin blocks of two sizes),
  * NB_SHARDED_STAGE, NB_FAIL_BUILDS / NB_FAIL_MERKLES (the next N device builds /
- * trees fail with NB_ERR_HIP).
+ * trees fail with NB_ERR_HIP).  Round 5 removed the switches of variants measured
+ * slower (NB_BIN_PIPE, NB_BIN_MIX, NB_BUCKET_GMAJOR = 0, NB_FINE_BITS = 19).
  * Unknown names: NB_ERR_ARG. */
 int nb_set_knob(const char *name, uint64_t value);
 int nb_get_knob(const char *name, uint64_t *value);

@@ -332,6 +332,12 @@ __global__ __launch_bounds__(kBlock) void bloom_probe_kernel(
 // bits, three rounds, instead of 915 of 2^20 bits, 3.57 rounds).  Tile boundaries
 // then fall inside filter words: the tile kernel ORs its two boundary words in with
 // 64-bit atomics (the bin kernel zeroes them first when the build overwrites).
+// Every single-level kernel finds a tile through `mul` (bin kernel, all its tails)
+// or tile_start (tile kernel), so any TileCfg -- counted or power-of-two -- is valid
+// on any single-level path (round 5: round 4's tails shifted by ts, and a counted
+// TileCfg that reached one needed a run-time refusal).  The two-level build and the
+// tiled probe construct power-of-two tilings of their own (choose_tiles /
+// super_tiles, probe_tiles): their re-bin and probe kernels shift.
 struct TileCfg {
     uint32_t ts;     // log2 bits per tile (counted tiles: the in-tile offset bits, 21)
     uint32_t T;      // number of tiles
@@ -343,16 +349,16 @@ struct TileCfg {
     uint32_t mul;    // tile of r = __umulhi(r, mul)
     uint32_t fmul;   // spill-flag tile of r = __umulhi(r, fmul) (the fts tiling)
     uint32_t w64;    // LDS words (u64) of one tile in the tile kernel, boundary words incl.
-    uint32_t mix = 0;  // bin kernel (KPT = 3, packed): blocks of two sizes, see bin_block_keys
-    uint32_t gmajor = 0;  // bucket layout: 0 [T][G][cap], 1 [G][T][cap] (bucket_region)
 };
 
-// First entry (in units of cap) of the bucket of tile t, shard g.  Shard g's runs
-// come from the bin blocks with blockIdx % G == g, which -- blocks go round-robin
-// over the 8 XCDs -- run on one XCD: shard-major buckets ([G][T]) keep each XCD's
-// scattered run writes inside its own 1/G of the bucket array instead of all of it.
+// First entry (in units of cap) of the bucket of tile t, shard g: buckets are laid
+// out shard-major, [G][T][cap].  Shard g's runs come from the bin blocks with
+// blockIdx % G == g, which -- blocks go round-robin over the 8 XCDs -- run on one
+// XCD, so each XCD's scattered run writes stay inside its own 1/G of the bucket
+// array (round 4: C4 1.46-1.50 -> 1.40-1.42 ms against the tile-major [T][G] layout,
+// profiles/r04_ab_gmajor_c4.txt; the tile-major layout was removed in round 5).
 __host__ __device__ inline uint32_t bucket_region(const TileCfg &tc, uint32_t t, uint32_t g) {
-    return tc.gmajor ? g * tc.T + t : t * tc.G + g;
+    return g * tc.T + t;
 }
 
 __host__ __device__ inline uint64_t tile_start(uint32_t t, uint32_t mul) {
@@ -693,7 +699,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
         Pack5 *bu = reinterpret_cast<Pack5 *>(buckets);
         for (uint32_t q = tid; q < units; q += NT) {
             const uint32_t *s5 = sorted + 5 * q;  // stride 5: conflict-free
-            const uint32_t a = s5[0], t = a >> tc.ts;
+            const uint32_t a = s5[0], t = __umulhi(a, tc.mul);
             if (!any_ovf || q < S4[t]) {
                 const uint32_t f0 = a & msk, f1 = s5[1] & msk, f2 = s5[2] & msk,
                                f3 = s5[3] & msk, f4 = s5[4] & msk;
@@ -774,7 +780,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
 #pragma unroll
                 for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) g[u] = NB_DIAG_WO == 2 ? 0u : GX[v[u] >> tc.ts];
+                for (int u = 0; u < 4; ++u) g[u] = NB_DIAG_WO == 2 ? 0u : GX[__umulhi(v[u], tc.mul)];
                 if (NB_DIAG_WO == 1) {  // diagnostic: LDS reads only
                     if ((v[0] ^ v[1] ^ v[2] ^ v[3] ^ g[0] ^ g[1] ^ g[2] ^ g[3]) == 0xFFFFFFFFu) bb[0] = 1;
                     continue;
@@ -786,7 +792,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
             }
             for (; j < total; j += NT) {
                 const uint32_t v = sorted[j];
-                *reinterpret_cast<ENTRY *>(bb + (GX[v >> tc.ts] + j * (uint32_t)sizeof(ENTRY))) = (ENTRY)v;
+                *reinterpret_cast<ENTRY *>(bb + (GX[__umulhi(v, tc.mul)] + j * (uint32_t)sizeof(ENTRY))) = (ENTRY)v;
             }
         } else if (!any_ovf) {  // buckets past 4 GiB: entry indices, 64-bit addresses
             uint32_t j = tid;
@@ -795,18 +801,18 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
 #pragma unroll
                 for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) g[u] = GX[v[u] >> tc.ts];
+                for (int u = 0; u < 4; ++u) g[u] = GX[__umulhi(v[u], tc.mul)];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) buckets[(uint32_t)(g[u] + j + u * NT)] = (ENTRY)v[u];
             }
             for (; j < total; j += NT) {
                 const uint32_t v = sorted[j];
-                buckets[(uint32_t)(GX[v >> tc.ts] + j)] = (ENTRY)v;
+                buckets[(uint32_t)(GX[__umulhi(v, tc.mul)] + j)] = (ENTRY)v;
             }
         } else {
             // overflow: entries past a bucket's capacity go to the spill bitmap
             for (uint32_t j = tid; j < total; j += NT) {
-                const uint32_t v = sorted[j], t = v >> tc.ts;
+                const uint32_t v = sorted[j], t = __umulhi(v, tc.mul);
                 if (j < S4[t]) {
                     buckets[(uint32_t)(GX[t] + j)] = (ENTRY)v;
                 } else {
@@ -1010,23 +1016,6 @@ struct BinPhase1 {
     }
 };
 
-// Blocks of two sizes (NB_BIN_MIX, KPT = 3): in every 16 consecutive blocks -- two
-// per XCD under round-robin dispatch -- the first 8 take KPT * NT keys and the last 8
-// (KPT - 1) * NT, so the two blocks resident on a CU run for different times and
-// their phases (hash, counting sort, write-out) drift apart instead of keeping step.
-// Returns the block's first key and trims *n to its last one.
-template <int KPT, int NT>
-__device__ __forceinline__ uint64_t bin_block_keys(uint32_t b, uint64_t *n) {
-    constexpr uint64_t big = (uint64_t)KPT * NT, small = (uint64_t)(KPT - 1) * NT;
-    const uint32_t g = b >> 4, r = b & 15;
-    const uint64_t base = (uint64_t)g * 8 * (big + small) + (r < 8 ? r * big : 8 * big + (r - 8) * small);
-    *n = min(*n, base + (r < 8 ? big : small));
-    return base;
-}
-__host__ __device__ constexpr uint64_t bin_mix_blocks(uint64_t n, uint64_t big, uint64_t small) {
-    return 16 * ((n + 8 * (big + small) - 1) / (8 * (big + small)));
-}
-
 // Two resident blocks per CU (8 waves per SIMD at NT = 1024): <= 64 VGPRs.
 #ifndef NB_BIN_MIN_WAVES
 #define NB_BIN_MIN_WAVES(NT) (2 * (NT) / 256)
@@ -1060,11 +1049,7 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
     // low 18 bits and the decode (cnt[t] - (A_t << 18)) >> 2 is exact.
     // register-loaded keys: their loads are issued first, in flight across the LDS
     // initialisation and its barrier
-    uint64_t base = (uint64_t)blockIdx.x * (KPT * NT);
-    if (KPT == 3 && tc.mix) {  // blocks of two sizes (NB_BIN_MIX): see bin_block_keys
-        base = bin_block_keys<KPT, NT>(blockIdx.x, &n);
-        if (base >= n) return;
-    }
+    const uint64_t base = (uint64_t)blockIdx.x * (KPT * NT);
     constexpr int kR = KR > 0 ? KR : 1;
     BinPhase1<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, KX> ph;
     ph.run(keys, offsets, key_len, n, c, tc.mul, T, cnt, sorted, wave_sums + NT / 64 + 1, base);
@@ -1124,7 +1109,7 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
 #pragma unroll
                     for (int j = 0; j < kR; ++j)
                         if (KX ? j < KX : j < (int)c.k)
-                            sorted[S[ridx[p][j] >> tc.ts] + ((rank[p][j] & kHandleMask) >> 2)] = ridx[p][j];
+                            sorted[S[__umulhi(ridx[p][j], tc.mul)] + ((rank[p][j] & kHandleMask) >> 2)] = ridx[p][j];
                 }
             }
 #pragma unroll
@@ -1158,13 +1143,13 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
                             r[u] = g.r;
                         }
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) q[u] = atomicAdd(&cnt[r[u] >> tc.ts], 1u);
+                        for (int u = 0; u < 4; ++u) q[u] = atomicAdd(&cnt[__umulhi(r[u], tc.mul)], 1u);
 #pragma unroll
                         for (int u = 0; u < 4; ++u) sorted[q[u]] = r[u];
                     }
                     for (; j < c.k; ++j) {
                         if (j) g.next(c);
-                        sorted[atomicAdd(&cnt[g.r >> tc.ts], 1u)] = g.r;
+                        sorted[atomicAdd(&cnt[__umulhi(g.r, tc.mul)], 1u)] = g.r;
                     }
                 }
             }
@@ -1195,13 +1180,13 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
 #pragma unroll
                 for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) g[u] = GX[v[u] >> tc.ts];
+                for (int u = 0; u < 4; ++u) g[u] = GX[__umulhi(v[u], tc.mul)];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) buckets[g[u] + j + u * NT] = (ENTRY)v[u];
             }
             for (; j < total; j += NT) {
                 const uint32_t v = sorted[j];
-                buckets[GX[v >> tc.ts] + j] = (ENTRY)v;
+                buckets[GX[__umulhi(v, tc.mul)] + j] = (ENTRY)v;
             }
             return;
         }
@@ -1212,7 +1197,7 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
             } else {
                 __hip_atomic_fetch_or(sc.spill32 + (v >> 5), 1u << (v & 31), __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT);
-                sc.spill_flag[v >> tc.fts] = 1u;
+                sc.spill_flag[__umulhi(v, tc.fmul)] = 1u;
             }
         };
         uint32_t j = tid;
@@ -1222,207 +1207,14 @@ __global__ __launch_bounds__(NT, NB_BIN_MIN_WAVES(NT)) void bloom_bin_kernel(
 #pragma unroll
             for (int u = 0; u < 4; ++u) v[u] = sorted[j + u * NT];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) gl[u] = GL[v[u] >> tc.ts];
+            for (int u = 0; u < 4; ++u) gl[u] = GL[__umulhi(v[u], tc.mul)];
 #pragma unroll
             for (int u = 0; u < 4; ++u) emit(j + u * NT, v[u], gl[u]);
         }
         for (; j < total; j += NT) {
             const uint32_t v = sorted[j];
-            emit(j, v, GL[v >> tc.ts]);
+            emit(j, v, GL[__umulhi(v, tc.mul)]);
         }
-    }
-}
-
-// Pipelined bin kernel (round 4) for 16-byte keys at k = KX with packed entries and
-// T <= 1 024 tiles (C4's shape).  The two-blocks-per-CU bin kernel runs its phases
-// one after the other in each block -- hash + count (VALU), scan + reservations,
-// placement (LDS), write-out (HBM stores) -- and the 512 resident blocks start
-// together, so the chip's write-outs bunch up.  Here one persistent 1 024-thread
-// block per CU holds two batches of 2 304 keys in LDS and overlaps them:
-//   A  waves 0-11 (H, 768 threads x 3 keys) hash batch i and count its indices into
-//      buffer i & 1, while waves 12-15 (S) write batch i-1's runs out of the other
-//      buffer;
-//   B  all 16 waves scan batch i's counts (one tile per thread) and reserve its runs;
-//   C  H places batch i; S resets the other buffer for batch i+1 (counters, run-pad
-//      sentinels, flags); each tile's owner writes its run table entry.
-// Run pads need no pass of their own: the sort area is filled with a sentinel
-// (0xFFFFFFFF, never an index) before the placement, and the write-out replaces a
-// sentinel slot by the first slot of its word (always a real entry of the same run).
-// The buckets, cursors and spill handling are the bin kernel's, so the tile kernel
-// is unchanged.  Four LDS-only barriers per batch (the write-out's stores stay in
-// flight across them).
-constexpr int kPipeThreads = 1024, kPipeH = 768, kPipeKPT = 3;
-constexpr uint32_t kPipeKPB = (uint32_t)kPipeH * kPipeKPT;  // keys per batch
-constexpr uint32_t kPipeMaxT = kPipeThreads;
-constexpr uint32_t kPipeMisc = 32;  // per buffer: [0, 16) wave sums, [16] slots, [17] overflow
-constexpr uint32_t kSortSentinel = 0xFFFFFFFFu;
-__host__ __device__ constexpr uint32_t pipe_sort_off(uint32_t T) { return (4 * T + 2 * kPipeMisc + 3) & ~3u; }
-__host__ __device__ constexpr uint32_t pipe_sort_words(uint32_t T, uint32_t kx) {
-    return (kPipeKPB * kx + 2 * T + 3) & ~3u;
-}
-__host__ __device__ constexpr size_t pipe_lds_bytes(uint32_t T, uint32_t kx) {
-    return ((size_t)pipe_sort_off(T) + 2 * (size_t)pipe_sort_words(T, kx)) * 4;
-}
-
-template <int FLAVOR, int KX>
-__global__ __launch_bounds__(kPipeThreads, 1) void bloom_bin_pipe_kernel(
-    const uint8_t *__restrict__ keys, uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc,
-    uint64_t *__restrict__ buckets) {
-    extern __shared__ uint32_t lds[];
-    const uint32_t T = tc.T, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const bool isH = tid < (uint32_t)kPipeH;
-    const uint32_t sort_off = pipe_sort_off(T), sort_words = pipe_sort_words(T, KX);
-    auto cnt_of = [&](uint32_t q) { return lds + q * T; };
-    auto gx_of = [&](uint32_t q) { return lds + (2 + q) * T; };
-    auto misc_of = [&](uint32_t q) { return lds + 4 * T + q * kPipeMisc; };
-    auto sort_of = [&](uint32_t q) { return lds + sort_off + q * sort_words; };
-    const uint32_t shard = blockIdx.x & (tc.G - 1);
-    uint32_t *cur = sc.gcur + (size_t)shard * T;
-    const uint64_t nbatch = (n + kPipeKPB - 1) / kPipeKPB;
-    const uint32_t nit = blockIdx.x < nbatch ? (uint32_t)((nbatch - blockIdx.x + gridDim.x - 1) / gridDim.x) : 0u;
-    if (sc.zero_words && tid == 0)  // counted tiles, overwrite: see TileCfg
-        for (uint32_t t = blockIdx.x + 1; t < T; t += gridDim.x) {
-            const uint64_t b = tile_start(t, tc.mul);
-            if (b & 63) sc.zero_words[b >> 6] = 0;
-        }
-    // buffer reset for a new batch: placement-handle counters, sentinels, flags
-    auto reset = [&](uint32_t q, uint32_t t0, uint32_t nthr) {
-        uint32_t *cq = cnt_of(q);
-        for (uint32_t t = t0; t < T; t += nthr) cq[t] = lds_addr(cq + t) << kHandleShift;
-        uint4 *s4 = reinterpret_cast<uint4 *>(sort_of(q));
-        const uint4 sent = make_uint4(kSortSentinel, kSortSentinel, kSortSentinel, kSortSentinel);
-        for (uint32_t w = t0; w < sort_words / 4; w += nthr) s4[w] = sent;
-        if (t0 == 0) misc_of(q)[17] = 0u;
-    };
-    reset(0, tid, kPipeThreads);
-    lds_barrier();
-
-    KeyBatch<FLAVOR, kFixed16, kPipeKPT> kb;
-    uint32_t ridx[kPipeKPT][KX], rank[kPipeKPT][KX];
-    auto batch_base = [&](uint32_t it) { return (uint64_t)(blockIdx.x + (uint64_t)it * gridDim.x) * kPipeKPB; };
-    if (isH && nit) kb.load(keys, nullptr, batch_base(0) + tid, kPipeH, n);
-    const uint32_t msk = (1u << tc.ts) - 1, hb = tc.ts - 11;
-    for (uint32_t it = 0; it <= nit; ++it) {
-        const uint32_t q = it & 1, p = q ^ 1;
-        const bool have = it < nit;
-        const uint64_t base = have ? batch_base(it) : 0;
-        // ---- A: H hashes + counts batch it into buffer q; S writes batch it-1 out of p
-        if (isH) {
-            if (have) {
-                uint32_t *cq = cnt_of(q);
-                uint64_t h1[kPipeKPT], h2[kPipeKPT];
-#pragma unroll
-                for (int k2 = 0; k2 < kPipeKPT; ++k2)
-                    kb.hash(c, keys, 16, base + (uint64_t)k2 * kPipeH + tid, k2, &h1[k2], &h2[k2]);
-#pragma unroll
-                for (int k2 = 0; k2 < kPipeKPT; ++k2)
-                    if (base + (uint64_t)k2 * kPipeH + tid < n) {
-                        IndexGen g;
-                        g.start(h1[k2], h2[k2], c);
-#pragma unroll
-                        for (int j = 0; j < KX; ++j) {
-                            if (j) g.next(c);
-                            ridx[k2][j] = g.r;
-                            rank[k2][j] = atomicAdd(&cq[__umulhi(g.r, tc.mul)], 4u);
-                        }
-                    }
-            }
-        } else if (it > 0) {
-            const uint32_t *sp = sort_of(p), *gp = gx_of(p), *mp = misc_of(p);
-            const uint32_t words = mp[16] / 3;
-            const bool ovf = mp[17] != 0u;
-            char *bb = reinterpret_cast<char *>(buckets);
-            for (uint32_t w = tid - kPipeH; w < words; w += kPipeThreads - kPipeH) {
-                const uint32_t a = sp[3 * w];
-                uint32_t b = sp[3 * w + 1], cc = sp[3 * w + 2];
-                b = b == kSortSentinel ? a : b;  // run pads: copies of the word's first entry
-                cc = cc == kSortSentinel ? a : cc;
-                const uint32_t t = __umulhi(a, tc.mul);
-                if (t >= T) continue;  // never (a word's first slot is a placed entry): no wild store
-                const uint32_t g = gp[t];
-                const uint32_t lo = (a & msk) | (b << 21);
-                const uint32_t hi = __builtin_amdgcn_ubfe(b, 11, hb) | ((cc & msk) << 10);
-                const uint64_t word = (uint64_t)hi << 32 | lo;
-                if (!ovf) {
-                    bucket_store(reinterpret_cast<uint64_t *>(bb + (g + w * 8u)), word);
-                } else {
-                    // pathological duplicates: a word past its bucket's capacity goes to
-                    // the spill bitmap (its position in the bucket from the run table)
-                    const uint32_t pos = (g + w * 8u) / 8u - bucket_region(tc, t, shard) * tc.cap;
-                    if (pos < tc.cap) {
-                        bucket_store(reinterpret_cast<uint64_t *>(bb + (g + w * 8u)), word);
-                    } else {
-                        const uint32_t v3[3] = {a, b, cc};
-                        for (int r = 0; r < 3; ++r) {
-                            __hip_atomic_fetch_or(sc.spill32 + (v3[r] >> 5), 1u << (v3[r] & 31), __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-                            sc.spill_flag[__umulhi(v3[r], tc.fmul)] = 1u;
-                        }
-                    }
-                }
-            }
-        }
-        lds_barrier();
-        if (!have) break;  // block-uniform: the last batch is written out
-        // ---- B: scan batch it's counts (thread t owns tile t), reserve its runs
-        uint32_t *cq = cnt_of(q), *mq = misc_of(q);
-        const uint32_t t = tid;
-        uint32_t h = 0;
-        if (t < T) h = (cq[t] - (lds_addr(cq + t) << kHandleShift)) >> 2;
-        const uint32_t local = (h + 2) / 3 * 3, incl = wave_inclusive_scan(local);
-        if (lane == 63) mq[wid] = incl;
-        lds_barrier();
-        const uint32_t wv = lane < kPipeThreads / 64 ? mq[lane] : 0u;
-        uint32_t before = lane < wid ? wv : 0u, all = wv;
-#pragma unroll
-        for (int o = 32; o; o >>= 1) {
-            before += __shfl_xor(before, o);
-            all += __shfl_xor(all, o);
-        }
-        const uint32_t st = before + incl - local;  // run start (slots)
-        const uint32_t u = (h + 2) / 3;             // run words
-        uint32_t ga = 0;
-        if (t < T) {
-            cq[t] = lds_addr(sort_of(q)) + 4 * st;
-            if (u) ga = atomicAdd(&cur[t], u);
-        }
-        if (tid == 0) mq[16] = all;
-        lds_barrier();
-        // ---- C: H places batch it; S resets buffer p for batch it+1; owners write
-        // the run table; H prefetches batch it+1's keys
-        if (isH) {
-            if (it + 1 < nit) {
-                KeyBatch<FLAVOR, kFixed16, kPipeKPT> nk;
-                nk.load(keys, nullptr, batch_base(it + 1) + tid, kPipeH, n);
-#pragma unroll
-                for (int k2 = 0; k2 < kPipeKPT; ++k2)
-                    if (base + (uint64_t)k2 * kPipeH + tid < n) {
-                        uint32_t s[KX];
-#pragma unroll
-                        for (int j = 0; j < KX; ++j) s[j] = lds_at(rank[k2][j] >> kHandleShift);
-#pragma unroll
-                        for (int j = 0; j < KX; ++j) lds_at(s[j] + (rank[k2][j] & kHandleMask)) = ridx[k2][j];
-                    }
-                kb = nk;
-            } else {
-#pragma unroll
-                for (int k2 = 0; k2 < kPipeKPT; ++k2)
-                    if (base + (uint64_t)k2 * kPipeH + tid < n) {
-                        uint32_t s[KX];
-#pragma unroll
-                        for (int j = 0; j < KX; ++j) s[j] = lds_at(rank[k2][j] >> kHandleShift);
-#pragma unroll
-                        for (int j = 0; j < KX; ++j) lds_at(s[j] + (rank[k2][j] & kHandleMask)) = ridx[k2][j];
-                    }
-            }
-        } else {
-            reset(p, tid - kPipeH, kPipeThreads - kPipeH);
-        }
-        if (t < T) {
-            gx_of(q)[t] = (bucket_region(tc, t, shard) * tc.cap + ga - st / 3) * 8u;
-            if ((uint64_t)ga + u > tc.cap) mq[17] = 1u;
-        }
-        lds_barrier();
     }
 }
 
@@ -2032,7 +1824,6 @@ using nb::knob;  // the A/B switches (nb_knobs.h): read once, atomics
 // C5: ts = 20, 4 096 fine tiles.
 TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     TileCfg tc;
-    tc.gmajor = knob(nb::kKnobBucketGMajor) != 0;
     uint32_t ts = 12;
     while (ts < 16 && ((uint64_t)m >> (ts + 1)) >= 1024) ++ts;
     while (ts < 20 && (((uint64_t)m + (1ull << ts) - 1) >> ts) > 2048) ++ts;
@@ -2070,15 +1861,19 @@ TileCfg choose_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
 // last round.  NB_TILE_COUNT: 0 this policy, 1 off, N > 1 exactly N tiles.  Entries
 // then hold 21-bit in-tile offsets (ts = 21: tiles < 2^21 bits with their boundary
 // words).  C4 / C3 (m = 958 505 838): 768 tiles, three rounds, instead of 915.
+// The CU count of the calling thread's current device, cached per device ID (a
+// process may build on devices of different sizes).
 uint32_t device_cus() {
-    static std::atomic<int> cus{0};
-    int v = cus.load(std::memory_order_relaxed);
+    constexpr int kMaxDev = 64;
+    static std::atomic<int> cus[kMaxDev];  // 0: not yet asked (static storage is zeroed)
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 256;
+    std::atomic<int> *slot = dev >= 0 && dev < kMaxDev ? &cus[dev] : nullptr;
+    int v = slot ? slot->load(std::memory_order_relaxed) : 0;
     if (!v) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
             v = 256;
-        cus.store(v, std::memory_order_relaxed);
+        if (slot) slot->store(v, std::memory_order_relaxed);
     }
     return (uint32_t)v;
 }
@@ -2111,20 +1906,6 @@ bool counted_tiles(uint32_t m, uint64_t n_chunk, uint32_t k, const TileCfg &p2, 
     tc.cap = cap_for(tc.T, tc.G, n_chunk, k);
     *out = tc;
     return true;
-}
-
-// The same tiling at a given tile size (NB_FINE_BITS: the two-level build's fine tiles).
-TileCfg retile(const TileCfg &base, uint32_t m, uint64_t n_chunk, uint32_t k, uint32_t ts) {
-    TileCfg tc = base;
-    tc.ts = tc.fts = ts;
-    tc.mul = tc.fmul = pow2_mul(ts);
-    tc.w64 = 1u << (ts - 6);
-    tc.T = (uint32_t)(((uint64_t)m + (1ull << ts) - 1) >> ts);
-    const double e = (double)n_chunk * k / ((double)tc.T * tc.G);
-    uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
-    cap = (cap + 7) & ~7ull;
-    tc.cap = (uint32_t)std::min<uint64_t>(cap, 0xFFFFFFC0ull);
-    return tc;
 }
 
 // Pass 1 of the two-level build: super tiles of kSuperFine fine tiles each.
@@ -2184,11 +1965,6 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
                    const FilterConsts &c, uint64_t *words, bool overwrite, hipStream_t st,
                    uint64_t chunk, const TileCfg &tc) {
     constexpr uint64_t kpb = (uint64_t)KPT * NT;
-    // counted tiles (a tile map other than a shift) exist only for the packed
-    // two-tile tail; anything else would find tiles by shifting and scatter out of
-    // range -- refuse it rather than launch it
-    if (tc.mul != pow2_mul(tc.ts) && !(sizeof(ENTRY) == 8 && KR > 0 && tc.T <= 2u * NT))
-        return fail(NB_ERR_ARG, "internal: counted tiles on a path that shifts");
     Workspace *ws;
     TileScratch sc;
     int rc;
@@ -2207,22 +1983,6 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(tile_ow, tile_lds)) ||
         (rc = allow_lds(tile_or, tile_lds)))
         return rc;
-    // the pipelined bin kernel for its shape (bloom_bin_pipe_kernel): 16-byte keys at
-    // k = KX, packed entries, batches of the same 2 304 keys (so the capacity the
-    // caller sized per block holds per batch), 385..1 024 tiles, buckets < 4 GiB
-    bool pipe = false;
-    uint32_t pipe_grid = 0;
-    const size_t pipe_lds = pipe_lds_bytes(tc.T, KX > 0 ? KX : 1);
-    if constexpr (LAYOUT == kFixed16 && sizeof(ENTRY) == 8 && KX > 0 && (uint64_t)KPT * NT == kPipeKPB) {
-        pipe = knob(nb::kKnobBinPipe) != 0 && tc.T <= kPipeMaxT && tc.T > kThreeBlockTiles &&
-               (uint64_t)tc.T * tc.G * tc.cap * sizeof(ENTRY) <= 0xFFFFFFFFull && pipe_lds <= 160 * 1024;
-        if (pipe) {
-            auto pk = bloom_bin_pipe_kernel<FLAVOR, KX>;
-            NB_HIP(hipFuncSetAttribute(reinterpret_cast<const void *>(pk),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)pipe_lds));
-            pipe_grid = device_cus();
-        }
-    }
     const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
     ENTRY *bk = reinterpret_cast<ENTRY *>(ws->buckets);
     for (uint64_t done = 0; done < n; done += chunk) {
@@ -2232,18 +1992,8 @@ int launch_tiled_e(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         TileScratch scb = sc;  // counted tiles, overwrite: the bin kernel zeroes the
                                // boundary words the tile kernel ORs into
         scb.zero_words = overwrite && done == 0 && tc.mul != pow2_mul(tc.ts) ? words : nullptr;
-        if constexpr (LAYOUT == kFixed16 && sizeof(ENTRY) == 8 && KX > 0 && (uint64_t)KPT * NT == kPipeKPB) {
-            if (pipe) {
-                const uint64_t nbatch = (cn + kPipeKPB - 1) / kPipeKPB;
-                hipLaunchKernelGGL((bloom_bin_pipe_kernel<FLAVOR, KX>),
-                                   dim3((uint32_t)std::min<uint64_t>(nbatch, pipe_grid)), dim3(kPipeThreads),
-                                   pipe_lds, st, ck, cn, c, tc, scb, reinterpret_cast<uint64_t *>(bk));
-            }
-        }
-        if (!pipe)
-            hipLaunchKernelGGL(bin,
-                               dim3((uint32_t)(tc.mix ? bin_mix_blocks(cn, kpb, kpb - NT) : (cn + kpb - 1) / kpb)),
-                               dim3(NT), bin_lds, st, ck, co, key_len, cn, c, tc, scb, bk);
+        hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT), bin_lds, st, ck, co,
+                           key_len, cn, c, tc, scb, bk);
         NB_HIP(hipGetLastError());
         hipLaunchKernelGGL((overwrite && done == 0) ? tile_ow : tile_or, dim3(tc.T),
                            dim3(kTileThreads), tile_lds, st, tc, sc, bk, words, nwords);
@@ -2422,16 +2172,6 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
         if (const uint64_t v = knob(nb::kKnobChunkKeys)) chunk = std::min<uint64_t>(n, v);
         tc = choose_tiles(c.fm.m, chunk, c.k);
         if constexpr (KR > 0) {
-            // NB_FINE_BITS = 19: 2^19-bit fine tiles (64 KB of LDS per tile block, so a
-            // tile block fits beside a bin or re-bin block), 64 per 2^25-bit super tile
-            const uint32_t fb = (uint32_t)knob(nb::kKnobFineBits);
-            if (fb == 19 && ((uint64_t)c.fm.m + (1u << 19) - 1) >> 19 <= kMaxCurTiles) {
-                const TileCfg t2 = retile(tc, c.fm.m, chunk, c.k, 19);
-                if (two_level_pack5())
-                    return launch_two_level<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, KX, Pack5>(
-                        keys, offsets, key_len, n, c, words, overwrite, st, chunk,
-                        super_tiles(t2, c.fm.m, chunk, c.k, 6), t2);
-            }
             if (two_level_pack5())  // 2^(ts+5)-bit super tiles: 25-bit offsets
                 return launch_two_level<FLAVOR, LAYOUT, KPT, NT, STAGE, KR, KX, Pack5>(
                     keys, offsets, key_len, n, c, words, overwrite, st, chunk,
@@ -2466,14 +2206,20 @@ int launch_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len,
             tc = ct;
         if (can_pack && tc.T <= 2u * NT && pk_lds_of(tc.T) <= 80 * 1024) {
             TileCfg tp = tc;
-            tp.mix = KPT == 3 && knob(nb::kKnobBinMix) != 0 ? 1u : 0u;
-            const uint64_t nblk = tp.mix ? bin_mix_blocks(chunk, kpb, kpb - NT) : (chunk + kpb - 1) / kpb;
+            const uint64_t nblk = (chunk + kpb - 1) / kpb;
             const uint64_t bps = (nblk + tc.G - 1) / tc.G;
             const uint64_t capw = ((uint64_t)tc.cap + 2 * bps + 2) / 3;
             tp.cap = (uint32_t)std::min<uint64_t>((capw + 7) & ~7ull, 0xFFFFFFC0ull);
             return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint64_t, NT, STAGE, KR, KX>(
                 keys, offsets, key_len, n, c, words, overwrite, st, chunk, tp);
         }
+    }
+    // 32-bit entries: power-of-two tiles by policy; an explicit tile count
+    // (NB_TILE_COUNT > 1) applies here too -- every single-level tail finds tiles
+    // through the TileCfg's multiplier (tests/test_gpu_buckets.py)
+    if (knob(nb::kKnobTileCount) > 1) {
+        TileCfg ct;
+        if (counted_tiles(c.fm.m, chunk, c.k, tc, &ct)) tc = ct;
     }
     return launch_tiled_e<FLAVOR, LAYOUT, KPT, uint32_t, NT, STAGE, KR, KX>(
         keys, offsets, key_len, n, c, words, overwrite, st, chunk, tc);
@@ -2586,7 +2332,6 @@ int launch_build_f(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
 // leaves >= 256 tiles; cap per (tile, shard) as the build's.
 TileCfg probe_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     TileCfg tc;
-    tc.gmajor = knob(nb::kKnobBucketGMajor) != 0;
     uint32_t ts = 12;
     while (ts < 20 && (((uint64_t)m + (1ull << (ts + 1)) - 1) >> (ts + 1)) >= 256) ++ts;
     tc.ts = ts;

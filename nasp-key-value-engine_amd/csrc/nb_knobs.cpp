@@ -25,9 +25,7 @@ constexpr KnobDef kDefs[nb::kKnobCount] = {
     {"NB_FIXED32", 1},       {"NB_FPMOD", 1},       {"NB_KEXACT", 1},
     {"NB_BIN_WIDE", 1},      {"NB_SHARDED_STAGE", 0},
     {"NB_OVERLAP", 6},       {"NB_SUBPASSES", 0},
-    {"NB_FINE_BITS", 0},     {"NB_TILE_COUNT", 0},
-    {"NB_BIN_PIPE", 0},      {"NB_BIN_MIX", 0},
-    {"NB_BUCKET_GMAJOR", 1},
+    {"NB_TILE_COUNT", 0},
     {"NB_PROBE_PATH", 0},    {"NB_PROBE_CHUNK", 0}, {"NB_PROBE_TILED_PCT", 30},
     {"NB_FAIL_BUILDS", 0},   {"NB_FAIL_MERKLES", 0},
 };

@@ -44,17 +44,9 @@ enum Knob : int {
                         //                   0: no pipelining
     kKnobSubpasses,     // NB_SUBPASSES      bin + re-bin sub-passes per tile pass (0: 2 for
                         //                   multi-pass builds, 1 for a single pass)
-    kKnobFineBits,      // NB_FINE_BITS      0: fine-tile policy (2^20 bits); 19: 2^19-bit fine
-                        //                   tiles in the two-level build
     kKnobTileCount,     // NB_TILE_COUNT     0: counted-tile policy (single-level packed path:
                         //                   a whole number of tile-kernel rounds), 1:
                         //                   power-of-two tiles only, else that many tiles
-    kKnobBinPipe,       // NB_BIN_PIPE       1: the pipelined bin kernel for 16-byte keys at
-                        //                   k = 7 over 385-1 024 tiles (C4); 0: off
-    kKnobBinMix,        // NB_BIN_MIX        1: bin blocks of two sizes (3 / 2 keys per thread)
-    kKnobBucketGMajor,  // NB_BUCKET_GMAJOR  1 (default): buckets laid out shard-major
-                        //                   ([G][T][cap]: one XCD's runs in 1/G of them),
-                        //                   0: tile-major ([T][G][cap])
     kKnobProbePath,     // NB_PROBE_PATH     0 auto | 1 "lane" (one lane per key) | 2 "tiled"
     kKnobProbeChunk,    // NB_PROBE_CHUNK    0: tiled-probe pass policy, else keys per pass
     kKnobProbeTiledPct, // NB_PROBE_TILED_PCT auto: the tiled path from this % of the sample

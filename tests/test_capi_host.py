@@ -153,20 +153,23 @@ def test_cpu_paths_read_only_key_bytes(built, oracle):
                                           np.ones(n, np.uint8))
 
 
-def test_round4_knob_defaults(built):
-    """Round 4's switches exist with their product defaults: the counted-tile policy
-    (NB_TILE_COUNT 0), the measured-slower bin variants off (NB_BIN_PIPE, NB_BIN_MIX 0)
-    and the sub-pass policy (NB_SUBPASSES 0: 2 for multi-pass builds, 1 for a single
-    pass), the tiled probe's pass policy (NB_PROBE_CHUNK 0), shard-major buckets
-    (NB_BUCKET_GMAJOR 1) and auto's tiled threshold (NB_PROBE_TILED_PCT 30) -- unless
-    the environment of this process set them."""
+def test_knob_defaults(built):
+    """The switches keep their product defaults: the counted-tile policy
+    (NB_TILE_COUNT 0), the sub-pass policy (NB_SUBPASSES 0: 2 for multi-pass builds, 1
+    for a single pass -- 0 is the policy, not one sub-pass), the tiled probe's pass
+    policy (NB_PROBE_CHUNK 0) and auto's tiled threshold (NB_PROBE_TILED_PCT 30) --
+    unless the environment of this process set them.  The switches of the variants
+    round 5 removed (measured slower) are refused as unknown names."""
     import nasp_bloom as nbm
-    for name in ("NB_TILE_COUNT", "NB_BIN_PIPE", "NB_BIN_MIX", "NB_SUBPASSES", "NB_PROBE_CHUNK"):
+    for name in ("NB_TILE_COUNT", "NB_SUBPASSES", "NB_PROBE_CHUNK"):
         if name not in os.environ:
             assert nbm.get_knob(name) == 0, name
-    if "NB_BUCKET_GMAJOR" not in os.environ:
-        assert nbm.get_knob("NB_BUCKET_GMAJOR") == 1
     if "NB_PROBE_TILED_PCT" not in os.environ:
         assert nbm.get_knob("NB_PROBE_TILED_PCT") == 30
-    with nbm.knobs(NB_TILE_COUNT=768, NB_BIN_PIPE=1):
-        assert nbm.get_knob("NB_TILE_COUNT") == 768 and nbm.get_knob("NB_BIN_PIPE") == 1
+    with nbm.knobs(NB_TILE_COUNT=768):
+        assert nbm.get_knob("NB_TILE_COUNT") == 768
+    for gone in ("NB_BIN_PIPE", "NB_BIN_MIX", "NB_BUCKET_GMAJOR", "NB_FINE_BITS"):
+        with pytest.raises(nbm.NaspBloomError):
+            nbm.get_knob(gone)
+        with pytest.raises(nbm.NaspBloomError):
+            nbm.set_knob(gone, 1)

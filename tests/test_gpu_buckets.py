@@ -1,10 +1,12 @@
-"""GPU parity of both bucket layouts (round 4, bloom_kernels.hip bucket_region):
-shard-major [G][T] (NB_BUCKET_GMAJOR=1, the default) and tile-major [T][G] (0), on
-every path that writes or reads buckets -- the single-level bin kernel
-(packed 21-bit and 32-bit entries, counted and power-of-two tiles, spill), the
-two-level build (pass-1 Pack5 units, re-bin, fine tiles), the pipelined bin kernel and
-the tiled probe in several key-range passes (NB_PROBE_CHUNK).  Bit-exact against the
-oracle (BloomFilter::add / possiblyContains, BloomFilter.cpp:67-86)."""
+"""GPU parity of every path that writes or reads the shard-major buckets
+(bloom_kernels.hip bucket_region, [G][T][cap]) -- the single-level bin kernel (packed
+21-bit and 32-bit entries, counted and power-of-two tiles, spill), the two-level build
+(pass-1 Pack5 units, re-bin, fine tiles) and the tiled probe in several key-range
+passes (NB_PROBE_CHUNK) -- and, since round 5, counted tiles on every single-level
+bin tail: round 4's unpacked tails found a tile by shifting, so a counted TileCfg that
+reached one scattered out of range and needed a run-time refusal; every tail now maps
+an index through the TileCfg's multiplier.  Bit-exact against the oracle
+(BloomFilter::add / possiblyContains, BloomFilter.cpp:67-86)."""
 import numpy as np
 import pytest
 
@@ -31,24 +33,29 @@ def build_into(dev, words_np, buf, offs, key_len, n, m, k, overwrite, flavor=0):
     return wt.cpu().numpy().view(np.uint64)
 
 
-# (m, k, key_len, extra knobs): counted tiles (C4's m), power-of-two tiles with 32-bit
-# entries, a C2-sized filter, the two-level build (C5's m, k = 10, several passes)
+# (m, k, key_len, extra knobs): counted tiles (C4's m, the packed two-tile tail), power-
+# of-two tiles with 32-bit entries, a C2-sized filter, the two-level build (C5's m,
+# k = 10, several passes); then counted tiles on the unpacked tails: 32-bit entries in
+# the two-tile tail (NB_PACK=0 with an explicit tile count), the general tail with
+# regenerated indices (NB_RANK=0), and k = 20 (> 16: no rank registers)
 CASES = [
     (958_505_838, 7, 16, {}),
     (958_505_838, 7, 16, {"NB_TILE_COUNT": "1", "NB_PACK": "0"}),
     (95_850_584, 7, 16, {"NB_CHUNK_KEYS": "70000"}),
     (2**32 - 1, 10, 32, {"NB_CHUNK_KEYS": "100000"}),
-    (958_505_838, 7, 16, {"NB_BIN_PIPE": "1"}),
+    (958_505_838, 7, 16, {"NB_TILE_COUNT": "701", "NB_PACK": "0"}),
+    (958_505_838, 7, 16, {"NB_TILE_COUNT": "1531", "NB_PACK": "0", "NB_RANK": "0"}),
+    (958_505_838, 20, 16, {"NB_TILE_COUNT": "997", "NB_PACK": "0"}),
+    (300_000_007, 7, 16, {"NB_TILE_COUNT": "333"}),
 ]
 
 
-@pytest.mark.parametrize("gmajor", ["0", "1"])
 @pytest.mark.parametrize("case", range(len(CASES)))
-def test_gmajor_build(dev, oracle, knobs, case, gmajor):
+def test_buckets_build(dev, oracle, knobs, case):
     from nasp_bloom import synth
     import nasp_bloom as nbm
     m, k, kl, extra = CASES[case]
-    knobs(NB_BUILD_PATH="tiled", NB_BUCKET_GMAJOR=gmajor, **extra)
+    knobs(NB_BUILD_PATH="tiled", **extra)
     n = 300_000
     buf = synth.fixed_keys(2 * n, kl, seed=31)
     stale = np.full(nbm.nwords(m), np.uint64(0xFFFFFFFFFFFFFFFF), np.uint64)
@@ -61,14 +68,16 @@ def test_gmajor_build(dev, oracle, knobs, case, gmajor):
     np.testing.assert_array_equal(got, oracle.build(1, vbuf, voffs, 0, n, m, k, SEED))
 
 
-@pytest.mark.parametrize("gmajor", ["0", "1"])
-@pytest.mark.parametrize("m,k,kl", [(958_505_838, 7, 16), (2**32 - 1, 10, 32)])
-def test_gmajor_spill(dev, oracle, knobs, m, k, kl, gmajor):
-    """Duplicated keys past the buckets' capacity (spill bitmap) in either layout,
-    then a normal build is exact again (cursors and spill scratch clean)."""
+@pytest.mark.parametrize("m,k,kl,extra", [(958_505_838, 7, 16, {}), (2**32 - 1, 10, 32, {}),
+                                          (958_505_838, 7, 16, {"NB_TILE_COUNT": "701", "NB_PACK": "0"}),
+                                          (958_505_838, 7, 16, {"NB_TILE_COUNT": "1531", "NB_RANK": "0"})])
+def test_buckets_spill(dev, oracle, knobs, m, k, kl, extra):
+    """Duplicated keys past the buckets' capacity (spill bitmap, folded per counted
+    or power-of-two tile), then a normal build is exact again (cursors and spill
+    scratch clean)."""
     from nasp_bloom import synth
     import nasp_bloom as nbm
-    knobs(NB_BUILD_PATH="tiled", NB_BUCKET_GMAJOR=gmajor, NB_CHUNK_KEYS="70000")
+    knobs(NB_BUILD_PATH="tiled", NB_CHUNK_KEYS="70000", **extra)
     stale = np.full(nbm.nwords(m), np.uint64(0xFFFFFFFFFFFFFFFF), np.uint64)
     n = 300_000
     dup = np.zeros(n * kl + 16, np.uint8)
@@ -80,22 +89,21 @@ def test_gmajor_spill(dev, oracle, knobs, m, k, kl, gmajor):
     np.testing.assert_array_equal(got, oracle.build(0, buf, None, kl, n, m, k, SEED))
 
 
-@pytest.mark.parametrize("gmajor", ["0", "1"])
 @pytest.mark.parametrize("chunk", ["0", "1000000"])
-def test_gmajor_tiled_probe(dev, oracle, knobs, gmajor, chunk):
-    """The tiled probe in either layout and in key-range passes: a filter of
-    60 % of 4.5M keys probed over all of them, bit-exact."""
+def test_buckets_tiled_probe(dev, oracle, knobs, chunk):
+    """The tiled probe in key-range passes: a filter of 60 % of 4.5M keys probed
+    over all of them, bit-exact."""
     import torch
     import nasp_bloom as nbm
-    from nasp_bloom import synth
     n, m, k, kl = 4_500_000, 958_505_838, 7, 16
+    from nasp_bloom import synth
     buf = synth.fixed_keys(n, kl, seed=33)
     npres = int(n * 0.6)
     wt = torch.zeros(nbm.nwords(m), dtype=torch.int64, device=dev)
     nbm.build_device(t_u8(buf, dev), None, kl, npres, m, k, SEED, 0, wt)
     torch.cuda.synchronize()
     words = wt.cpu().numpy().view(np.uint64)
-    knobs(NB_PROBE_PATH="tiled", NB_BUCKET_GMAJOR=gmajor, NB_PROBE_CHUNK=chunk)
+    knobs(NB_PROBE_PATH="tiled", NB_PROBE_CHUNK=chunk)
     got = dev_probe(dev, buf, None, kl, n, m, k, SEED, words, 0)
     np.testing.assert_array_equal(got, oracle.probe(0, buf, None, kl, n, m, k, SEED, words))
     assert got[:npres].all()

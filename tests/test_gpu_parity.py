@@ -457,19 +457,18 @@ def test_two_level_overflow_spill(dev, oracle, knobs):
     np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("overlap,fine,sub", [("1", "0", "1"), ("2", "0", "2"), ("6", "0", "3"),
-                                              ("0", "0", "3"), ("0", "19", "1"), ("2", "19", "2")])
-def test_two_level_overlap(dev, oracle, overlap, fine, sub, knobs):
+@pytest.mark.parametrize("overlap,sub", [("1", "1"), ("2", "2"), ("6", "3"), ("0", "3"), ("6", "1"),
+                                         ("2", "5")])
+def test_two_level_overlap(dev, oracle, overlap, sub, knobs):
     """NB_OVERLAP: the two-level sub-passes pipelined over two streams (a re-bin
     beside the next bin kernel; & 4: a tile kernel beside the next pass's bin kernel;
     sub-pass- and pass-parity scratch); NB_SUBPASSES: bin + re-bin sub-passes sharing
-    one tile pass; NB_FINE_BITS = 19: 8 192 fine tiles of 2^19 bits, 64 per super
-    tile.  Odd and even pass counts, overwrite over stale words, duplicated keys
+    one tile pass.  Odd and even pass counts, overwrite over stale words, duplicated keys
     spilling in every pass, and an exact normal build afterwards (scratch clean)."""
     import torch
     import nasp_bloom as nbm
     from nasp_bloom import synth
-    knobs(NB_BUILD_PATH="tiled", NB_OVERLAP=overlap, NB_FINE_BITS=fine, NB_SUBPASSES=sub)
+    knobs(NB_BUILD_PATH="tiled", NB_OVERLAP=overlap, NB_SUBPASSES=sub)
     m, k = 2**32 - 1, 10
     n = 700_001
     buf = synth.fixed_keys(n, 32, seed=91)
@@ -488,7 +487,7 @@ def test_two_level_overlap(dev, oracle, overlap, fine, sub, knobs):
     vb, vo = synth.var_keys(300_000)
     got = dev_build(dev, vb, vo, 0, 300_000, m, k, SEED)
     np.testing.assert_array_equal(got, oracle.build(0, vb, vo, 0, 300_000, m, k, SEED))
-    knobs(NB_OVERLAP="0", NB_FINE_BITS="0", NB_SUBPASSES="1")
+    knobs(NB_OVERLAP="0", NB_SUBPASSES="1")
     got = dev_build(dev, buf, None, 32, n, m, k, SEED)
     np.testing.assert_array_equal(got, want)
 

@@ -11,9 +11,10 @@
 //   4. a chunked pipeline: bin kernels on (256 - x) CUs beside tile kernels on x
 //      CUs, checked bit for bit against the one-shot build.
 //   5. power-of-two (915) vs counted (768) tiles, one-shot builds interleaved.
-//   6. cstops / layout: phase stops in the product configuration (counted tiles,
-//      shard-major buckets), and tile-major vs shard-major buckets interleaved.
-// usage: ubench_c4 [all|stops|cstops|layout|tiles|mask|pipe]
+//   6. cstops: phase stops in the product configuration (counted tiles, shard-major
+//      buckets).  (Round 4's `layout` mode -- tile-major vs shard-major buckets -- went
+//      with the tile-major layout in round 5; profiles/r04_c4_layout.txt is its output.)
+// usage: ubench_c4 [all|stops|cstops|tiles|mask|pipe]
 #include <hip/hip_runtime.h>
 __constant__ int g_diag_stop;
 #define NB_DIAG_STOP(phase) (g_diag_stop == (phase) || ((phase) == 1 && g_diag_stop == 11))
@@ -259,10 +260,9 @@ int main(int argc, char **argv) {
         }
     }
 
-    if (all || !strcmp(what, "cstops") || !strcmp(what, "layout")) {
-        // the product's configuration: counted tiles (768), shard-major buckets unless
-        // NB_BUCKET_GMAJOR=0.  cstops: phase stops of the bin kernel and the tile
-        // kernel alone; layout: tile-major vs shard-major buckets, interleaved
+    if (all || !strcmp(what, "cstops")) {
+        // the product's configuration: counted tiles (768), shard-major buckets; phase
+        // stops of the bin kernel and the tile kernel alone
         TileCfg p2 = choose_tiles(kM, kN, kK), ct;
         if (!counted_tiles(kM, kN, kK, p2, &ct)) { printf("counted tiles: policy declined\n"); return 1; }
         {
@@ -285,7 +285,7 @@ int main(int argc, char **argv) {
                                dim3(kTileThreads), (size_t)tc.w64 * 8 + (2 * kShards + 1) * 4, s0, tc, s.sc[0],
                                s.bk[0], s.words, nwords);
         };
-        printf("product config: counted T=%u, %s buckets\n", ct.T, ct.gmajor ? "shard-major" : "tile-major");
+        printf("product config: counted T=%u, shard-major buckets\n", ct.T);
         for (int r = 0; r < 20; ++r) {  // settle the clock
             bin(ct);
             tile(ct);
@@ -324,35 +324,6 @@ int main(int argc, char **argv) {
                 if (r >= 1) sum += t;
             }
             printf("tile kernel: best %.4f  mean(5) %.4f ms\n", best, sum / 5);
-        }
-        if (!strcmp(what, "layout") || all) {
-            float bb[2] = {1e30f, 1e30f}, tt[2] = {1e30f, 1e30f}, sum[2] = {0, 0};
-            for (int r = 0; r < 10; ++r)
-                for (int v = 0; v < 2; ++v) {
-                    TileCfg tc = ct;
-                    tc.gmajor = (uint32_t)v;
-                    CK(hipMemsetAsync(s.words, 0xA5, nwords * 8, s0));
-                    Ev e, f;
-                    CK(hipEventRecord(e.a, s0));
-                    bin(tc);
-                    CK(hipEventRecord(e.b, s0));
-                    CK(hipEventRecord(f.a, s0));
-                    tile(tc);
-                    CK(hipEventRecord(f.b, s0));
-                    const float b = e.ms(), t = f.ms();
-                    bb[v] = std::min(bb[v], b);
-                    tt[v] = std::min(tt[v], t);
-                    if (r >= 2) sum[v] += b + t;
-                    if (r == 9) {
-                        std::vector<uint64_t> a(nwords), ref(nwords);
-                        CK(hipMemcpy(a.data(), s.words, nwords * 8, hipMemcpyDeviceToHost));
-                        CK(hipMemcpy(ref.data(), s.words_ref, nwords * 8, hipMemcpyDeviceToHost));
-                        printf("%s buckets: %s\n", v ? "shard-major" : "tile-major", a == ref ? "bit-exact" : "MISMATCH");
-                    }
-                }
-            for (int v = 0; v < 2; ++v)
-                printf("%s buckets: bin best %.4f, tile best %.4f, build mean(8) %.4f ms\n",
-                       v ? "shard-major" : "tile-major", bb[v], tt[v], sum[v] / 8);
         }
     }
 

@@ -207,7 +207,7 @@ int main(int argc, char **argv) {
     }
     if (c3 && argc > 2 && !strcmp(argv[2], "product")) {
         // C3 in the product's configuration (launch_tiled: counted tiles, k = 7
-        // exact, shard-major buckets unless NB_BUCKET_GMAJOR=0): phase stops of the
+        // exact, shard-major buckets): phase stops of the
         // staged bin kernel after a settle, then the tile kernel
         TileCfg p2 = choose_tiles(m, n, k), ct;
         if (!counted_tiles(m, n, k, p2, &ct)) ct = p2;
@@ -228,7 +228,7 @@ int main(int argc, char **argv) {
         const size_t tlds = (size_t)ct.w64 * 8 + (2 * kShards + 1) * 4;
         allow_lds(tile, tlds);
         printf("C3 product: T=%u mul=%u cap=%u words, %s buckets, bin LDS %zu B\n", ct.T, ct.mul, ct.cap,
-               ct.gmajor ? "shard-major" : "tile-major", lds);
+               "shard-major", lds);
         auto bin = [&]() {
             hipLaunchKernelGGL(kern, dim3((uint32_t)((n + kpb - 1) / kpb)), dim3(NT), lds, 0, keys, g_offsets, 0u,
                                n, c, ct, scz, (uint64_t *)buckets);
