@@ -606,8 +606,10 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     const uint32_t total = wave_sums[kWaves];
     if (scan_wave) {
         const uint32_t st0 = wave_sums[wid] + incl - local, st1 = st0 + slots(h0);
-        if (t0 < T) cnt[t0] = sort_b + 4 * st0;
-        if (t0 + 1 < T) cnt[t0 + 1] = sort_b + 4 * st1;
+        // the run start less the counter's handle base (mod 2^32): a placement handle
+        // pk = A_t << 18 | 4 rank plus cnt[t] is the slot's LDS address -- one add
+        if (t0 < T) cnt[t0] = sort_b + 4 * st0 - ((lds0 + 4 * t0) << kHandleShift);
+        if (t0 + 1 < T) cnt[t0 + 1] = sort_b + 4 * st1 - ((lds0 + 4 * t0 + 4) << kHandleShift);
     }
     __syncthreads();
     if (NB_DIAG_STOP(2)) return;
@@ -628,7 +630,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
             if (base + (uint64_t)p * NT + tid < n) {
 #pragma unroll
                 for (int j = 0; j < KR; ++j)
-                    if (KX ? j < KX : j < (int)k) lds_at(st[p][j] + (pk[p][j] & kHandleMask)) = ridx[p][j];
+                    if (KX ? j < KX : j < (int)k) lds_at(st[p][j] + pk[p][j]) = ridx[p][j];
             }
     } else
 #pragma unroll
@@ -641,13 +643,13 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
                     if (KX ? j < KX : j < (int)k) st[j] = lds_at(pk[p][j] >> kHandleShift);
 #pragma unroll
                 for (int j = 0; j < KR; ++j)
-                    if (KX ? j < KX : j < (int)k) lds_at(st[j] + (pk[p][j] & kHandleMask)) = ridx[p][j];
+                    if (KX ? j < KX : j < (int)k) lds_at(st[j] + pk[p][j]) = ridx[p][j];
             } else {
 #pragma unroll
                 for (int j = 0; j < KR; ++j)
                     if (KX ? j < KX : j < (int)k) {
                         const uint32_t h = pk[p][j];
-                        lds_at(lds_at(h >> kHandleShift) + (h & kHandleMask)) = ridx[p][j];
+                        lds_at(lds_at(h >> kHandleShift) + h) = ridx[p][j];
                     }
             }
         }
@@ -663,7 +665,7 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
     const bool b32 = PK < 5 && (uint64_t)T * tc.G * tc.cap * sizeof(ENTRY) <= 0xFFFFFFFFull;
     const uint32_t esz = (b32 && !any_ovf) ? (uint32_t)sizeof(ENTRY) : 1u;
     auto run_entry = [&](uint32_t t, uint32_t g, uint32_t h) {
-        uint32_t st = (cnt[t] - sort_b) / 4;
+        uint32_t st = (cnt[t] + ((lds0 + 4 * t) << kHandleShift) - sort_b) / 4;
         if (PACK) {  // 0..PK-1 pad slots (straight-line: the compiler would emit a memset loop)
             uint32_t *run = lds + sort_off_words + st;
             const uint32_t np = slots(h) - h;

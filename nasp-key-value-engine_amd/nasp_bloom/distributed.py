@@ -49,12 +49,13 @@ def _hip_merge(dst: torch.Tensor, recv: torch.Tensor, nsrc: int, stride: int) ->
     or_merge_device(dst, recv, dst.numel(), nsrc, stride)
 
 
-def _mark(marks: list | None, name: str, device) -> None:
+def _mark(marks: list | None, name: str, device, stream=None) -> None:
     """Phase boundary of an instrumented step (bench.py's N > 1 diagnostics): a timing
-    event recorded on the current stream of `device`, appended as (name, event)."""
+    event recorded on `stream` (default: the current stream of `device`), appended as
+    (name, event)."""
     if marks is not None and torch.device(device).type == "cuda":
         ev = torch.cuda.Event(enable_timing=True)
-        ev.record(torch.cuda.current_stream(device))
+        ev.record(stream if stream is not None else torch.cuda.current_stream(device))
         marks.append((name, ev))
 
 
@@ -134,12 +135,18 @@ def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len:
         partial[nwords(m):].zero_()
     else:  # a test-side builder may OR into the words
         partial = torch.zeros(world * S, dtype=torch.int64, device=keys.device)
-    _mark(marks, "start", keys.device)
+    # the build runs on `stream` when one is given; the merge's collectives and OR
+    # kernel on the current stream, which waits for the build first (a caller's
+    # non-current build stream is joined, not raced)
+    side = stream is not None and keys.is_cuda and stream != torch.cuda.current_stream(keys.device)
+    _mark(marks, "start", keys.device, stream if side else None)
     if build_fn is None:
         build_device(keys, offsets, key_len, n, m, k, seed, flavor, partial, stream=stream,
                      overwrite=True)
     else:
         build_fn(keys, offsets, key_len, n, m, k, seed, flavor, partial)
+    if side:
+        torch.cuda.current_stream(keys.device).wait_stream(stream)
     _mark(marks, "build", keys.device)
     out = merge_partials(partial, m, group=group, all_gather=all_gather and host_out is None,
                          merge_fn=merge_fn, exchange_single=exchange_single,
@@ -150,7 +157,7 @@ def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len:
         host_out[: out.numel()].copy_(out, non_blocking=host_out.is_pinned())
         if host_out.is_pinned() and out.is_cuda:
             # the copy is asynchronous: wait for it before the host words are handed
-            # back
+            # back -- so bench.py's host_ending phase is a synchronous D2H
             landed = torch.cuda.Event()
             landed.record(torch.cuda.current_stream(out.device))
             landed.synchronize()

@@ -783,6 +783,18 @@ def test_cooperative_build_single_rank(dev, oracle):
         torch.cuda.synchronize()
         got = full.cpu().numpy().view(np.uint64)
         np.testing.assert_array_equal(got[: want.size], want)
+    # the build on a caller's non-current stream: the merge (on the current stream)
+    # joins it before the exchange; the phase marks bracket the build on that stream
+    side = torch.cuda.Stream(device=dev)
+    keys = t_u8(buf, dev)
+    torch.cuda.synchronize()
+    marks = []
+    full = D.build_cooperative(keys, None, 32, n, synth.C5.m, synth.C5.k, SEED, 0, exchange_single=True,
+                               stream=side, marks=marks)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(full.cpu().numpy().view(np.uint64)[: want.size], want)
+    ph = D.phase_ms(marks)
+    assert ph["build"] > 0 and set(ph) >= {"build", "all_to_all", "or_merge", "all_gather"}
     dist.destroy_process_group()
 
 

@@ -32,16 +32,32 @@ def main():
     ap.add_argument("--batches", default="present,absent,mixed")
     ap.add_argument("--no-lane", action="store_true")
     ap.add_argument("--auto-pct", default="", help="auto path at these NB_PROBE_TILED_PCT values")
+    ap.add_argument("--workload", default="c4", choices=["c4", "c5"],
+                    help="c4: C4's filter from the 100M probed present keys; c5: C5's shape "
+                         "(m = 2^32-1, k = 10, 32-byte keys), --n probed keys, the filter built "
+                         "from --fill-keys device-random keys (the present keys among them)")
+    ap.add_argument("--n", type=int, default=50_000_000)
+    ap.add_argument("--fill-keys", type=int, default=400_000_000)
     args = ap.parse_args()
     reps = args.reps
-    wl = synth.C4
     dev = torch.device("cuda", 0)
     st = torch.cuda.Stream(device=dev)
-    p_np, _, kl = synth.keys_for(wl)
-    a_np, _, _ = synth.keys_for(wl, seed=synth.SEED + 1000)
-    # (the generator's buffers keep their tail padding: kernels may read past a key)
-    present = torch.from_numpy(p_np).to(dev)
-    absent = torch.from_numpy(a_np).to(dev)
+    fill = None
+    if args.workload == "c4":
+        wl = synth.C4
+        p_np, _, kl = synth.keys_for(wl)
+        a_np, _, _ = synth.keys_for(wl, seed=synth.SEED + 1000)
+        # (the generator's buffers keep their tail padding: kernels may read past a key)
+        present = torch.from_numpy(p_np).to(dev)
+        absent = torch.from_numpy(a_np).to(dev)
+    else:
+        wl = synth.Workload("c5_shape_probe", args.n, 32, synth.C5.m, synth.C5.k, 0.01)
+        kl = 32
+        g = torch.Generator(device=dev)
+        g.manual_seed(5)
+        fill = torch.randint(0, 256, (args.fill_keys * kl + 64,), dtype=torch.uint8, device=dev, generator=g)
+        present = fill[:wl.n * kl + 64].clone()
+        absent = torch.randint(0, 256, (wl.n * kl + 64,), dtype=torch.uint8, device=dev, generator=g)
     mixed = present.clone()
     mv = mixed[:wl.n * kl].view(wl.n, kl)
     mv[1::2] = absent[:wl.n * kl].view(wl.n, kl)[1::2]
@@ -53,9 +69,17 @@ def main():
         batches[f"p{pc}"] = b
     batches = {b: batches[b] for b in args.batches.split(",")}
     words = torch.zeros(nbm.nwords(wl.m), dtype=torch.int64, device=dev)
-    nbm.build_device(present, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, stream=st,
-                     overwrite=True)
+    if fill is None:
+        nbm.build_device(present, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, stream=st,
+                         overwrite=True)
+    else:
+        nbm.build_device(fill, None, kl, args.fill_keys, wl.m, wl.k, synth.H2_SEED, 0, words, stream=st,
+                         overwrite=True)
+        del fill
     torch.cuda.synchronize(dev)
+    ones = int(np.unpackbits(words.view(torch.uint8)[:1 << 20].cpu().numpy()).sum())
+    print(f"{wl.name}: n={wl.n} m={wl.m} k={wl.k} key_len={kl}, filter fill ~{ones / (8 << 20):.3f} "
+          f"(first MiB)", flush=True)
     out = torch.empty(wl.n, dtype=torch.uint8, device=dev)
     ref = {}
     with nbm.knobs(NB_PROBE_PATH="lane"):
@@ -86,7 +110,7 @@ def main():
                     table.setdefault((label, name), []).append(ms)
                     print(f"rep {rep} {label:>16} {name:>8} {ms:8.3f} ms  {wl.n / ms / 1e6:7.2f} Gkeys/s",
                           flush=True)
-    print("summary (ms per 100M-key call, wall clock over 5 calls; min over reps):")
+    print(f"summary (ms per {wl.n / 1e6:.0f}M-key call, wall clock over 5 calls; min over reps):")
     for label, _, _, _ in variants:
         print(f"  {label:>16} " + "  ".join(f"{n} {min(table[(label, n)]):7.3f}" for n in batches))
     print(f"answers identical to the lane path: {'yes' if bad == 0 else f'NO ({bad} mismatches)'}")
