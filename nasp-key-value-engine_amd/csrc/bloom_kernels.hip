@@ -835,14 +835,22 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
 // generator's start state (6 registers per key) is kept and the placement
 // regenerates the indices.  kid[p]: the key (index in the launch) slot p of this
 // lane hashed -- staged variable-length keys are hashed in a permuted order.
-template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR, int KX = 0>
+// The split tiled probe (round 5) counts a range of each key's indices: J0 is the
+// first one counted (the earlier ones only advance the generator; KX, when set, is
+// the end), and with GATE a key is counted only while gate[kid] != 0 (its answer
+// after the first round); live[p] says whether slot p was counted.
+template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR, int KX = 0, int J0 = 0,
+          bool GATE = false>
 struct BinPhase1 {
     static constexpr int kR = KR > 0 ? KR : 1;
     static_assert(KR == 0 || (uint64_t)KPT * NT * KR < (1u << (kHandleShift - 2)),
                   "a block's ranks must fit the placement handle's low bits");
+    static_assert(J0 == 0 || KR > 0, "an index range needs the rank registers");
     IndexGen gen[KPT];
     uint32_t ridx[KPT][kR], rank[KPT][kR];
     uint32_t kid[KPT];  // (mod 2^32: the probe launches chunks of < 2^32 keys)
+    bool live[KPT];
+    const uint8_t *gate = nullptr;
 
     __device__ __forceinline__ void run(const uint8_t *__restrict__ keys,
                                         const uint64_t *__restrict__ offsets, uint32_t key_len,
@@ -852,6 +860,16 @@ struct BinPhase1 {
         const uint32_t tid = threadIdx.x;
         KeyBatch<FLAVOR, LAYOUT, KPT> kb;
         if (!STAGE) kb.load(keys, offsets, base + tid, NT, n);
+        if (!STAGE) {  // (issued with the key loads: the gate bytes are read before the hash)
+#pragma unroll
+            for (int p = 0; p < KPT; ++p) {
+                const uint64_t i = base + (uint64_t)p * NT + tid;
+                live[p] = i < n && (!GATE || gate[(uint32_t)i] != 0);
+            }
+        } else {
+#pragma unroll
+            for (int p = 0; p < KPT; ++p) live[p] = false;
+        }
         for (uint32_t t = tid; t < T; t += NT) cnt[t] = KR > 0 ? lds_addr(cnt + t) << kHandleShift : 0u;
         if (tid == 0) *any_flag = 0u;  // block_any's flag
         if (STAGE && tid < kLenClasses)  // the staged keys' length-class counters (see below)
@@ -871,8 +889,10 @@ struct BinPhase1 {
                 for (int j = 0; j < kR; ++j) {
                     if (KX ? j < KX : j < (int)c.k) {
                         if (j) g.next(c);
-                        ridx[p][j] = g.r;
-                        rank[p][j] = NB_DIAG_NOCOUNT ? g.r : atomicAdd(&cnt[__umulhi(g.r, tmul)], 4u);
+                        if (j >= J0) {
+                            ridx[p][j] = g.r;
+                            rank[p][j] = NB_DIAG_NOCOUNT ? g.r : atomicAdd(&cnt[__umulhi(g.r, tmul)], 4u);
+                        }
                     }
                 }
             } else {
@@ -892,7 +912,7 @@ struct BinPhase1 {
                 kb.hash(c, keys, key_len, base + (uint64_t)p * NT + tid, p, &h1[p], &h2[p]);
 #pragma unroll
             for (int p = 0; p < KPT; ++p)
-                if (base + (uint64_t)p * NT + tid < n) count_key(p, h1[p], h2[p]);
+                if (live[p]) count_key(p, h1[p], h2[p]);
 #pragma unroll
             for (int p = 0; p < KPT; ++p) kid[p] = (uint32_t)(base + (uint64_t)p * NT + tid);
         } else {
@@ -981,6 +1001,8 @@ struct BinPhase1 {
                     kid[p] = (uint32_t)(pb + src);
                     if (tid < kLenClasses) lhist[tid] = 0u;  // read by all before the barrier above
                 }
+                if (GATE && kvalid) kvalid = gate[kid[p]] != 0;
+                live[p] = kvalid;
                 if (kvalid) {
                     uint64_t h1, h2;
                     const uint32_t len = klen;
@@ -1513,7 +1535,10 @@ __host__ __device__ constexpr uint32_t probe_sort_offset_words(uint32_t T) {
     return (4 * T + 32 + 3) & ~3u;  // cnt | S | GX | L | wave_sums, 16-byte aligned
 }
 
-template <int FLAVOR, int LAYOUT, bool STAGE, int KR>
+// Split probe (round 5): J0..J1 (J1 = 0: k) is the range of each key's indices this
+// launch bins; R2 marks the second round, which bins only the keys whose answer the
+// first round left at 1 and leaves the answers' initialisation to the first.
+template <int FLAVOR, int LAYOUT, bool STAGE, int KR, int J0 = 0, int J1 = 0, bool R2 = false>
 __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) void probe_bin_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
     uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc, uint64_t *__restrict__ buckets,
@@ -1527,10 +1552,11 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
     uint32_t *sidx = lds + probe_sort_offset_words(T);  // [NT * k] indices, sorted by tile
     uint32_t *skid = sidx + NT * k;                     // [NT * k] their keys
     const uint64_t base = (uint64_t)blockIdx.x * NT;
-    BinPhase1<FLAVOR, LAYOUT, 1, NT, STAGE, KR> ph;
+    BinPhase1<FLAVOR, LAYOUT, 1, NT, STAGE, KR, J1, J0, R2> ph;
+    if (R2) ph.gate = out;
     ph.run(keys, offsets, key_len, n, c, tc.mul, T, cnt, sidx, wave_sums + NT / 64 + 1, base);
     const bool valid = base + tid < n;  // (staged keys: the valid ones fill the first slots)
-    if (valid) out[ph.kid[0]] = 1;
+    if (!R2 && valid) out[ph.kid[0]] = 1;
     // counts from the placement handles (A_t << kHandleShift | 4 rank, see BinPhase1)
     for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << kHandleShift)) >> 2;
     __syncthreads();
@@ -1545,10 +1571,10 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
         L[t] = S[t] + (g < tc.cap ? tc.cap - g : 0u);
     }
     // placement (the reservations' round trips overlap it)
-    if (valid) {
+    if (ph.live[0]) {
 #pragma unroll
-        for (int j = 0; j < KR; ++j)
-            if (j < (int)k) {
+        for (int j = J0; j < KR; ++j)
+            if (J1 ? j < J1 : j < (int)k) {
                 const uint32_t pos = S[ph.ridx[0][j] >> tc.ts] + ((ph.rank[0][j] & kHandleMask) >> 2);
                 sidx[pos] = ph.ridx[0][j];
                 skid[pos] = ph.kid[0];
@@ -2376,10 +2402,18 @@ int launch_probe_lane(const uint8_t *keys, const uint64_t *offsets, uint32_t key
     return NB_OK;
 }
 
+// The split tiled probe's first round: each key's first kSplitJ indices.
+constexpr int kSplitJ = 2;
+
+// split: two rounds per pass -- the first bins every key's first kSplitJ indices and
+// answers the keys with a zero among them, the second bins the other k - kSplitJ
+// indices of the keys still at 1.  An absent key costs ~1 miss store
+// in the first round and, one time in four (filter half full), ~(k - 2) / 2 in the
+// second, instead of ~k/2; a present key costs the same k entries and two hashes.
 template <int FLAVOR, int LAYOUT, int KR>
 int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                        const FilterConsts &c, const uint64_t *words, uint8_t *out, hipStream_t st,
-                       const ProbeGate &gate) {
+                       const ProbeGate &gate, bool split = false) {
     constexpr bool STAGE = !vec_layout(LAYOUT);
     constexpr int NT = kProbeThreads;
     Workspace *ws;
@@ -2399,20 +2433,28 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
     if (bin_lds > kMaxBlockLds) return fail(NB_ERR_UNSUPPORTED, "tiled probe: LDS of the shape");
     const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
     auto bin = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR>;
+    auto bin1 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, kSplitJ, false>;
+    auto bin2 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, kSplitJ, 0, true>;
     auto tile = probe_tile_kernel<kTileThreads>;
-    if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(tile, tile_lds))) return rc;
+    split = split && c.k > (uint32_t)kSplitJ;
+    if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(bin1, bin_lds)) || (rc = allow_lds(bin2, bin_lds)) ||
+        (rc = allow_lds(tile, tile_lds)))
+        return rc;
     const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
     uint64_t *bk = reinterpret_cast<uint64_t *>(ws->buckets);
     for (uint64_t done = 0; done < n; done += chunk) {
         const uint64_t cn = std::min(chunk, n - done);
         const uint8_t *ck = offsets ? keys : keys + done * key_len;
         const uint64_t *co = offsets ? offsets + done : nullptr;
-        hipLaunchKernelGGL(bin, dim3((uint32_t)((cn + NT - 1) / NT)), dim3(NT), bin_lds, st, ck, co,
-                           key_len, cn, c, tc, sc, bk, words, out + done, gate);
-        NB_HIP(hipGetLastError());
-        hipLaunchKernelGGL(tile, dim3(tc.T), dim3(kTileThreads), tile_lds, st, tc, sc,
-                           (const uint64_t *)bk, words, nwords, out + done, gate);
-        NB_HIP(hipGetLastError());
+        for (int round = 0; round < (split ? 2 : 1); ++round) {
+            auto b = !split ? bin : round == 0 ? bin1 : bin2;
+            hipLaunchKernelGGL(b, dim3((uint32_t)((cn + NT - 1) / NT)), dim3(NT), bin_lds, st, ck, co,
+                               key_len, cn, c, tc, sc, bk, words, out + done, gate);
+            NB_HIP(hipGetLastError());
+            hipLaunchKernelGGL(tile, dim3(tc.T), dim3(kTileThreads), tile_lds, st, tc, sc,
+                               (const uint64_t *)bk, words, nwords, out + done, gate);
+            NB_HIP(hipGetLastError());
+        }
     }
     return NB_OK;
 }
@@ -2435,16 +2477,17 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     if (path == 1 || !tiled_ok || (path == 0 && n < kProbeTiledMin))
         return launch_probe_lane<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, out, st, none);
     auto tiled = [&](const uint8_t *k_, const uint64_t *o_, uint64_t n_, uint8_t *out_,
-                     const ProbeGate &g) -> int {
+                     const ProbeGate &g, bool split = false) -> int {
         if constexpr (kTiledLayout) {
             if (c.k <= 8)
-                return launch_probe_tiled<FLAVOR, LAYOUT, 8>(k_, o_, key_len, n_, c, words, out_, st, g);
+                return launch_probe_tiled<FLAVOR, LAYOUT, 8>(k_, o_, key_len, n_, c, words, out_, st, g, split);
             if constexpr (LAYOUT == kFixed32)
-                return launch_probe_tiled<FLAVOR, LAYOUT, 16>(k_, o_, key_len, n_, c, words, out_, st, g);
+                return launch_probe_tiled<FLAVOR, LAYOUT, 16>(k_, o_, key_len, n_, c, words, out_, st, g,
+                                                              split);
         }
         return fail(NB_ERR_UNSUPPORTED, "tiled probe: unsupported shape");
     };
-    if (path == 2) return tiled(keys, offsets, n, out, none);
+    if (path == 2 || path == 3) return tiled(keys, offsets, n, out, none, path == 3);
     // auto: the sample (one key per lane, one count per block).  Outside stream
     // capture its 16 counts come back to the host (one 64-byte copy and a stream
     // synchronisation) and only the chosen path is launched; under capture both

@@ -40,6 +40,7 @@ uint64_t parse(int id, const char *s) {
     if (id == nb::kKnobProbePath) {
         if (!std::strcmp(s, "lane")) return 1;
         if (!std::strcmp(s, "tiled")) return 2;
+        if (!std::strcmp(s, "split")) return 3;
         if (!std::strcmp(s, "auto")) return 0;
     }
     return std::strtoull(s, nullptr, 10);

@@ -48,6 +48,7 @@ enum Knob : int {
                         //                   a whole number of tile-kernel rounds), 1:
                         //                   power-of-two tiles only, else that many tiles
     kKnobProbePath,     // NB_PROBE_PATH     0 auto | 1 "lane" (one lane per key) | 2 "tiled"
+                        //                   | 3 "split" (the tiled probe in two rounds)
     kKnobProbeChunk,    // NB_PROBE_CHUNK    0: tiled-probe pass policy, else keys per pass
     kKnobProbeTiledPct, // NB_PROBE_TILED_PCT auto: the tiled path from this % of the sample
                         //                   present (default 30; 50 before round 4's end)

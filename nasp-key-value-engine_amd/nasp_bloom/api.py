@@ -43,7 +43,7 @@ def std_hash(data: bytes, flavor: int = FLAVOR_LIBSTDCXX) -> int:
 
 # named values of the path knobs (include/nasp_bloom.h nb_set_knob)
 _KNOB_NAMES = {"NB_BUILD_PATH": {"auto": 0, "atomic": 1, "tiled": 2},
-               "NB_PROBE_PATH": {"auto": 0, "lane": 1, "tiled": 2}}
+               "NB_PROBE_PATH": {"auto": 0, "lane": 1, "tiled": 2, "split": 3}}
 
 
 def set_knob(name: str, value) -> None:

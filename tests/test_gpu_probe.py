@@ -1,8 +1,9 @@
 """GPU parity of the batch probe (BloomFilter::possiblyContains, BloomFilter.cpp:67-80,
 callers SSTManager.cpp:203,224) on every path: the lane kernel (one lane per key,
 early exit), the tiled path (probe_bin_kernel + probe_tile_kernel: lookups binned by
-filter tile and tested in LDS) and auto (a sampled prefix picks the path on the
-device).  Bit-exact against oracle.probe on mixed present / absent batches; the
+filter tile and tested in LDS), the split tiled path (round 5: two rounds, the
+second over the keys the first one's two indices left at 1) and auto (a sampled
+prefix picks the path on the device).  Bit-exact against oracle.probe on mixed present / absent batches; the
 tiled and lane answers equal each other at C4's full size."""
 import numpy as np
 import pytest
@@ -51,7 +52,7 @@ def probe_shapes():
     return shapes()
 
 
-@pytest.mark.parametrize("path", ["lane", "tiled", "auto"])
+@pytest.mark.parametrize("path", ["lane", "tiled", "split", "auto"])
 @pytest.mark.parametrize("shape", ["c4_fixed16", "c3_varlen", "c2_fixed16_fnv", "c5_fixed32_k10"])
 @pytest.mark.parametrize("present_first", [True, False])
 def test_probe_paths_match_oracle(dev, oracle, knobs, probe_shapes, path, shape, present_first):
@@ -77,15 +78,17 @@ def test_probe_paths_match_oracle(dev, oracle, knobs, probe_shapes, path, shape,
     assert got.mean() - 0.6 < 0.02  # the absent 40 %: false positives only
 
 
-def test_tiled_probe_overflow_and_small_filter(dev, oracle, knobs):
+@pytest.mark.parametrize("path", ["tiled", "split"])
+def test_tiled_probe_overflow_and_small_filter(dev, oracle, knobs, path):
     """Duplicated keys overflow the probe's buckets (those entries are tested in the
-    bin kernel instead); a small filter (few, small tiles); k = 1 and k = 8."""
+    bin kernel instead); a small filter (few, small tiles); k = 1 (the split path
+    then runs one round), k = 3 and k = 8."""
+    knobs(NB_PROBE_PATH=path)
     from nasp_bloom import synth
-    knobs(NB_PROBE_PATH="tiled")
     n = 400_000
     dup = np.zeros(n * 16 + 16, np.uint8)
     dup[: 16 * 1000] = synth.fixed_keys(1000, 16)[: 16 * 1000]
-    for m, k in ((958_505_838, 7), (1_000_003, 8), (2**20 + 5, 1)):
+    for m, k in ((958_505_838, 7), (1_000_003, 8), (2**20 + 5, 1), (3_000_017, 3)):
         words = oracle.build(0, dup, None, 16, 2000, m, k, SEED)  # 1000 distinct + zero keys
         got = dev_probe(dev, dup, None, 16, n, m, k, SEED, words)
         np.testing.assert_array_equal(got, oracle.probe(0, dup, None, 16, n, m, k, SEED, words))
@@ -109,7 +112,7 @@ def test_tiled_probe_c4_full_size(dev, knobs):
     words = torch.zeros(nbm.nwords(w.m), dtype=torch.int64, device=dev)
     nbm.build_device(kt, None, 16, w.n, w.m, w.k, SEED, 0, words, overwrite=True)
     outs = {}
-    for path in ("tiled", "lane"):
+    for path in ("tiled", "split", "lane"):
         knobs(NB_PROBE_PATH=path)
         out = torch.zeros(2 * w.n, dtype=torch.uint8, device=dev)
         nbm.probe_device(kt, None, 16, 2 * w.n, w.m, w.k, SEED, 0, words, out)
@@ -117,11 +120,12 @@ def test_tiled_probe_c4_full_size(dev, knobs):
         outs[path] = out
     assert int(outs["tiled"][: w.n].min()) == 1
     assert torch.equal(outs["tiled"], outs["lane"])
+    assert torch.equal(outs["split"], outs["lane"])
     fp = float(outs["lane"][w.n:].float().mean())
     assert 0.008 < fp < 0.012
 
 
-@pytest.mark.parametrize("path", ["tiled", "auto"])
+@pytest.mark.parametrize("path", ["tiled", "split", "auto"])
 @pytest.mark.parametrize("k", [11, 12, 16])
 def test_probe_32byte_keys_large_k_full_filter(dev, oracle, knobs, path, k):
     """32-byte keys at k = 11..16 over m = 2^32 - 1 (4 096 probe tiles): the tiled bin

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--chunks", default="0,25000000,12500000,6250000,3125000")
     ap.add_argument("--batches", default="present,absent,mixed")
     ap.add_argument("--no-lane", action="store_true")
+    ap.add_argument("--split", action="store_true", help="also the split tiled probe (two rounds)")
     ap.add_argument("--auto-pct", default="", help="auto path at these NB_PROBE_TILED_PCT values")
     ap.add_argument("--workload", default="c4", choices=["c4", "c5"],
                     help="c4: C4's filter from the 100M probed present keys; c5: C5's shape "
@@ -62,7 +63,10 @@ def main():
     mv = mixed[:wl.n * kl].view(wl.n, kl)
     mv[1::2] = absent[:wl.n * kl].view(wl.n, kl)[1::2]
     batches = {"present": present, "absent": absent, "mixed": mixed}
-    for pc in (20, 30, 40):  # pc % present: keys i with i % 10 < pc / 10 (the sample sees the same mix)
+    want_b = args.batches.split(",")
+    for pc in range(10, 100, 10):  # pc % present: keys i with i % 10 < pc / 10 (the sample sees the same mix)
+        if f"p{pc}" not in want_b:
+            continue
         b = absent.clone()
         bv, pv = b[:wl.n * kl].view(wl.n // 10, 10, kl), present[:wl.n * kl].view(wl.n // 10, 10, kl)
         bv[:, :pc // 10] = pv[:, :pc // 10]
@@ -89,7 +93,8 @@ def main():
             ref[name] = out.clone()
     variants = ([] if args.no_lane else [("lane", "lane", 0, "30")]) + [
         (f"tiled C={c / 1e6 if c else 'policy'}M", "tiled", c, "30") for c in map(int, args.chunks.split(",") if args.chunks else [])
-    ] + [(f"auto pct={p}", "auto", 0, p) for p in filter(None, args.auto_pct.split(","))]
+    ] + ([("split", "split", 0, "30")] if args.split else []) + [
+        (f"auto pct={p}", "auto", 0, p) for p in filter(None, args.auto_pct.split(","))]
     table = {}
     bad = 0
     for rep in range(reps):

@@ -7,8 +7,12 @@
 //   pofs    the same, the second half of the grid starting with a half batch, so
 //           the two blocks sharing a CU run half a batch out of phase (one hashes --
 //           VALU -- while the other sorts -- LDS)
+//   s2, s4  the build in 2 / 4 key chunks: every bin kernel on one stream, every tile
+//           kernel on a second, high-priority stream (chunk i's tile kernel beside
+//           chunk i+1's bin kernel; no CU masks -- the dispatcher interleaves the two
+//           kernels' workgroups as CUs free up), two bucket sets alternating
 // Each build is checked bit for bit against the product's one-shot build.
-// usage: ubench_r05 [rounds]
+// usage: ubench_r05 [rounds] [variants, e.g. prod,s2,s4]
 #include <hip/hip_runtime.h>
 
 #include "../nasp-key-value-engine_amd/csrc/bloom_kernels.hip"
@@ -16,6 +20,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                 \
@@ -94,11 +99,12 @@ struct Ev {
 int main(int argc, char **argv) {
     setvbuf(stdout, nullptr, _IONBF, 0);
     const int rounds = argc > 1 ? atoi(argv[1]) : 10;
+    const std::string want = argc > 2 ? argv[2] : "prod,pers,pofs,s2,s4";
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     uint8_t *keys;
-    uint64_t *words, *words_ref, *bk;
-    uint32_t *zeroed;
+    uint64_t *words, *words_ref, *bk[2];
+    uint32_t *zeroed[2];
     CK(hipMalloc(&keys, kN * 16 + 64));
     const uint64_t nwords = ((uint64_t)kM + 63) / 64;
     CK(hipMalloc(&words, nwords * 8));
@@ -107,13 +113,15 @@ int main(int argc, char **argv) {
     FilterConsts c = nb::make_consts(kM, kK, 17027509906831645879ull, 0);
     nb::set_fixed_len(c, 16);
     const size_t zb = (kCurWords + kFlagWords + kSuperCurWords + 2 * nwords) * 4;
-    CK(hipMalloc(&zeroed, zb));
-    CK(hipMemset(zeroed, 0, zb));
-    TileScratch sc;
-    sc.gcur = zeroed;
-    sc.spill_flag = zeroed + kCurWords;
-    sc.spill32 = zeroed + kCurWords + kFlagWords + kSuperCurWords;
-    sc.zero_words = words;
+    TileScratch sc[2];
+    for (int q = 0; q < 2; ++q) {
+        CK(hipMalloc(&zeroed[q], zb));
+        CK(hipMemset(zeroed[q], 0, zb));
+        sc[q].gcur = zeroed[q];
+        sc[q].spill_flag = zeroed[q] + kCurWords;
+        sc[q].spill32 = zeroed[q] + kCurWords + kFlagWords + kSuperCurWords;
+        sc[q].zero_words = nullptr;
+    }
     // the product's tiling for C4; capacity in words for the most runs any variant makes
     TileCfg p2 = choose_tiles(kM, kN, kK), ct;
     if (!counted_tiles(kM, kN, kK, p2, &ct)) { printf("counted tiles: policy declined\n"); return 1; }
@@ -124,77 +132,121 @@ int main(int argc, char **argv) {
         const uint64_t capw = ((uint64_t)ct.cap + 2 * bps + 2) / 3;
         ct.cap = (uint32_t)((capw + 7) & ~7ull);
     }
-    CK(hipMalloc(&bk, (size_t)ct.T * ct.G * ct.cap * 8));
+    for (int q = 0; q < 2; ++q) CK(hipMalloc(&bk[q], (size_t)ct.T * ct.G * ct.cap * 8));
     const size_t bin_lds = (size_t)bin_sort_offset_words(ct.T) * 4 + kKPB * kK * 4 + (size_t)ct.T * 8;
     const size_t tile_lds = (size_t)ct.w64 * 8 + (2 * kShards + 1) * 4;
     for (const void *k : {reinterpret_cast<const void *>(BIN), reinterpret_cast<const void *>(PERS),
                           reinterpret_cast<const void *>(POFS)})
         CK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bin_lds));
-    CK(hipFuncSetAttribute(reinterpret_cast<const void *>(bloom_tile_or_kernel<uint64_t, true>),
-                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)tile_lds));
+    for (const void *k : {reinterpret_cast<const void *>(bloom_tile_or_kernel<uint64_t, true>),
+                          reinterpret_cast<const void *>(bloom_tile_or_kernel<uint64_t, false>)})
+        CK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)tile_lds));
     printf("C4: n=%llu m=%u k=%u T=%u G=%u cap=%u words, bin LDS %zu B, tile LDS %zu B, CUs %d, P %u\n",
            (unsigned long long)kN, kM, kK, ct.T, ct.G, ct.cap, bin_lds, tile_lds, cus, P);
-    hipStream_t s0;
+    hipStream_t s0, s1;
     CK(hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
-    auto bin = [&](int v) {
-        if (v == 0)
-            hipLaunchKernelGGL(BIN, dim3((uint32_t)((kN + kKPB - 1) / kKPB)), dim3(kNT), bin_lds, s0, keys,
-                               nullptr, 16u, kN, c, ct, sc, bk);
-        else if (v == 1)
-            hipLaunchKernelGGL(PERS, dim3(P), dim3(kNT), bin_lds, s0, keys, nullptr, 16u, kN, c, ct, sc, bk);
+    int lo = 0, hi = 0;
+    CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    CK(hipStreamCreateWithPriority(&s1, hipStreamNonBlocking, hi));
+    hipEvent_t ev_bin[2], ev_tile[2];
+    for (int q = 0; q < 2; ++q) {
+        CK(hipEventCreateWithFlags(&ev_bin[q], hipEventDisableTiming));
+        CK(hipEventCreateWithFlags(&ev_tile[q], hipEventDisableTiming));
+    }
+    auto bin_k = [&](int v, int q, uint64_t first, uint64_t cn, uint64_t *zw, hipStream_t st) {
+        TileScratch s = sc[q];
+        s.zero_words = zw;
+        const uint8_t *kk = keys + first * 16;
+        if (v == 1)
+            hipLaunchKernelGGL(PERS, dim3(P), dim3(kNT), bin_lds, st, kk, nullptr, 16u, cn, c, ct, s, bk[q]);
+        else if (v == 2)
+            hipLaunchKernelGGL(POFS, dim3(P), dim3(kNT), bin_lds, st, kk, nullptr, 16u, cn, c, ct, s, bk[q]);
         else
-            hipLaunchKernelGGL(POFS, dim3(P), dim3(kNT), bin_lds, s0, keys, nullptr, 16u, kN, c, ct, sc, bk);
+            hipLaunchKernelGGL(BIN, dim3((uint32_t)((cn + kKPB - 1) / kKPB)), dim3(kNT), bin_lds, st, kk,
+                               nullptr, 16u, cn, c, ct, s, bk[q]);
         CK(hipGetLastError());
     };
-    auto tile = [&](uint64_t *w) {
-        hipLaunchKernelGGL((bloom_tile_or_kernel<uint64_t, true>), dim3(ct.T), dim3(kTileThreads), tile_lds, s0,
-                           ct, sc, bk, w, nwords);
+    auto tile_k = [&](int q, bool ow, uint64_t *w, hipStream_t st) {
+        auto k = ow ? bloom_tile_or_kernel<uint64_t, true> : bloom_tile_or_kernel<uint64_t, false>;
+        hipLaunchKernelGGL(k, dim3(ct.T), dim3(kTileThreads), tile_lds, st, ct, sc[q], bk[q], w, nwords);
         CK(hipGetLastError());
+    };
+    // one build of variant v into w (all work ends on s0)
+    auto build = [&](int v, uint64_t *w) {
+        if (v <= 2) {
+            bin_k(v, 0, 0, kN, w, s0);
+            tile_k(0, true, w, s0);
+            return;
+        }
+        const int C = v == 3 ? 2 : 4;
+        const uint64_t chunk = (kN / C + kKPB - 1) / kKPB * kKPB;
+        CK(hipEventRecord(ev_tile[1], s0));  // s1 starts after everything on s0
+        CK(hipStreamWaitEvent(s1, ev_tile[1], 0));
+        int i = 0;
+        for (uint64_t first = 0; first < kN; first += chunk, ++i) {
+            const uint64_t cn = std::min(chunk, kN - first);
+            const int q = i & 1;
+            if (i >= 2) CK(hipStreamWaitEvent(s0, ev_tile[q], 0));  // buckets q free
+            bin_k(0, q, first, cn, i == 0 ? w : nullptr, s0);
+            CK(hipEventRecord(ev_bin[q], s0));
+            CK(hipStreamWaitEvent(s1, ev_bin[q], 0));
+            tile_k(q, i == 0, w, s1);
+            CK(hipEventRecord(ev_tile[q], s1));
+        }
+        CK(hipStreamWaitEvent(s0, ev_tile[(i - 1) & 1], 0));
     };
     // reference (product) filter, then settle the clock
-    sc.zero_words = words_ref;
-    bin(0);
-    tile(words_ref);
-    sc.zero_words = words;
+    build(0, words_ref);
     CK(hipStreamSynchronize(s0));
-    for (int r = 0; r < 25; ++r) {
-        bin(0);
-        tile(words);
-    }
+    for (int r = 0; r < 25; ++r) build(0, words);
     CK(hipStreamSynchronize(s0));
-    const char *names[] = {"prod", "pers", "pofs"};
-    const int NV = 3;
-    std::vector<float> tb[NV], tt[NV];
-    bool ok[NV] = {true, true, true};
+    const char *names[] = {"prod", "pers", "pofs", "s2", "s4"};
+    std::vector<int> vs;
+    for (int v = 0; v < 5; ++v)
+        if (("," + want + ",").find(std::string(",") + names[v] + ",") != std::string::npos) vs.push_back(v);
+    std::vector<float> tb[5], tt[5];
+    bool ok[5] = {true, true, true, true, true};
     std::vector<uint64_t> a(nwords), ref(nwords);
     CK(hipMemcpy(ref.data(), words_ref, nwords * 8, hipMemcpyDeviceToHost));
     for (int r = 0; r < rounds; ++r)
-        for (int v = 0; v < NV; ++v) {
+        for (int v : vs) {
             CK(hipMemsetAsync(words, 0xA5, nwords * 8, s0));
             Ev e, f;
             CK(hipEventRecord(e.a, s0));
-            bin(v);
-            CK(hipEventRecord(e.b, s0));
-            CK(hipEventRecord(f.a, s0));
-            tile(words);
-            CK(hipEventRecord(f.b, s0));
-            tb[v].push_back(e.ms());
-            tt[v].push_back(f.ms());
+            if (v <= 2) {
+                bin_k(v, 0, 0, kN, words, s0);
+                CK(hipEventRecord(e.b, s0));
+                CK(hipEventRecord(f.a, s0));
+                tile_k(0, true, words, s0);
+                CK(hipEventRecord(f.b, s0));
+                tb[v].push_back(e.ms());
+                tt[v].push_back(f.ms());
+            } else {
+                build(v, words);
+                CK(hipEventRecord(e.b, s0));
+                tb[v].push_back(e.ms());
+                tt[v].push_back(0.f);
+            }
             if (r == 0 || r == rounds - 1) {
+                CK(hipStreamSynchronize(s0));
                 CK(hipMemcpy(a.data(), words, nwords * 8, hipMemcpyDeviceToHost));
                 ok[v] = ok[v] && a == ref;
             }
         }
-    for (int v = 0; v < NV; ++v) {
+    for (int v : vs) {
         std::vector<float> x = tb[v], y = tt[v];
         std::sort(x.begin(), x.end());
         std::sort(y.begin(), y.end());
         double sb = 0, st = 0;
         for (float q : tb[v]) sb += q;
         for (float q : tt[v]) st += q;
-        printf("%s: bin min %.4f med %.4f mean %.4f | tile min %.4f med %.4f | build mean %.4f ms  %s\n",
-               names[v], x[0], x[x.size() / 2], sb / x.size(), y[0], y[y.size() / 2], (sb + st) / x.size(),
-               ok[v] ? "bit-exact" : "MISMATCH");
+        if (v <= 2)
+            printf("%s: bin min %.4f med %.4f mean %.4f | tile min %.4f med %.4f | build mean %.4f ms  %s\n",
+                   names[v], x[0], x[x.size() / 2], sb / x.size(), y[0], y[y.size() / 2], (sb + st) / x.size(),
+                   ok[v] ? "bit-exact" : "MISMATCH");
+        else
+            printf("%s: build min %.4f med %.4f mean %.4f ms  %s\n", names[v], x[0], x[x.size() / 2], sb / x.size(),
+                   ok[v] ? "bit-exact" : "MISMATCH");
     }
     CK(hipDeviceSynchronize());
     printf("done\n");
