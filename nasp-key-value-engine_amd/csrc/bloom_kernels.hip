@@ -254,22 +254,32 @@ struct ProbeGate {
                              // choice they make == want
     uint32_t blocks;         // sample blocks (words of decide)
     uint32_t sample;         // keys in the sample
-    uint32_t want;           // 1 the lane path, 2 the tiled path
+    uint32_t want;           // 1 the lane path, 2 the tiled path, 3 the split tiled path
     uint32_t pct = 30;       // tiled from this percentage of the sample present on
+    uint32_t split_pct = 101;  // the split path from this percentage (> 100: never) up
+                               // to kSplitTiledPct, where the tiled path takes over
 };
-// Auto's choice from the sample's hit count h of s keys: tiled when at least pct %
-// were present (a present key costs the lane kernel ~k gathers, an
-// absent one ~2, and the tiled path a fixed pass plus ~k/2 stores per absent key;
-// on C3 / C4's filter the two break even at 28-30 % present)
-__host__ __device__ inline bool probe_pick_tiled(uint64_t h, uint64_t s, uint32_t pct) {
-    return 100 * h >= (uint64_t)pct * s;
+// Where the split path hands over to the one-round tiled path (on C4's
+// filter the two cross at ~50 % present, profiles/r05_probe_split_c4.txt)
+constexpr uint32_t kSplitTiledPct = 50;
+// Auto's choice from the sample's hit count h of s keys: 1 lane, 2 tiled, 3 split.
+// Without the split path: tiled when at least pct % were present (a present key costs
+// the lane kernel ~k gathers, an absent one ~2, and the tiled path a fixed pass plus
+// ~k/2 miss stores per absent key; on C3 / C4's filter and on C5's shape the two break
+// even at ~30 % present).  With it (k <= 8): lane below split_pct %, split up to
+// kSplitTiledPct %, tiled from there.
+__host__ __device__ inline uint32_t probe_pick(uint64_t h, uint64_t s, uint32_t pct, uint32_t split_pct) {
+    if (split_pct <= 100) {
+        if (100 * h < (uint64_t)split_pct * s) return 1u;
+        return 100 * h < (uint64_t)kSplitTiledPct * s ? 3u : 2u;
+    }
+    return 100 * h >= (uint64_t)pct * s ? 2u : 1u;
 }
 __device__ __forceinline__ bool gate_open(const ProbeGate &g) {
     if (!g.decide) return true;
     uint32_t h = 0;  // uniform: scalar loads
     for (uint32_t b = 0; b < g.blocks; ++b) h += g.decide[b];
-    const uint32_t choice = probe_pick_tiled(h, g.sample, g.pct) ? 2u : 1u;
-    return choice == g.want;
+    return probe_pick(h, g.sample, g.pct, g.split_pct) == g.want;
 }
 
 // One lane per key, k gathers with an early exit at the first zero bit.
@@ -838,9 +848,12 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
 // The split tiled probe (round 5) counts a range of each key's indices: J0 is the
 // first one counted (the earlier ones only advance the generator; KX, when set, is
 // the end), and with GATE a key is counted only while gate[kid] != 0 (its answer
-// after the first round); live[p] says whether slot p was counted.
+// after the first round); live[p] says whether slot p was counted.  ST = 1: the first
+// round also stores each key's index state after its KX indices (state[kid] = {next
+// index, the two biased step sizes, the wrap bit of every later step}); ST = 2: the
+// second round reads that state instead of loading and hashing the key.
 template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR, int KX = 0, int J0 = 0,
-          bool GATE = false>
+          bool GATE = false, int ST = 0>
 struct BinPhase1 {
     static constexpr int kR = KR > 0 ? KR : 1;
     static_assert(KR == 0 || (uint64_t)KPT * NT * KR < (1u << (kHandleShift - 2)),
@@ -851,6 +864,7 @@ struct BinPhase1 {
     uint32_t kid[KPT];  // (mod 2^32: the probe launches chunks of < 2^32 keys)
     bool live[KPT];
     const uint8_t *gate = nullptr;
+    uint4 *state = nullptr;  // ST > 0: [keys of the launch] index state between the rounds
 
     __device__ __forceinline__ void run(const uint8_t *__restrict__ keys,
                                         const uint64_t *__restrict__ offsets, uint32_t key_len,
@@ -858,6 +872,36 @@ struct BinPhase1 {
                                         uint32_t *cnt, uint32_t *sorted, uint32_t *any_flag,
                                         uint64_t base) {
         const uint32_t tid = threadIdx.x;
+        if constexpr (ST == 2) {  // the second round: no key loads, no hash
+            static_assert(KR > 0 && GATE, "the state round counts gated index ranges");
+            uint4 sv[KPT];
+#pragma unroll
+            for (int p = 0; p < KPT; ++p) {
+                const uint64_t i = base + (uint64_t)p * NT + tid;
+                kid[p] = (uint32_t)i;
+                live[p] = i < n && gate[(uint32_t)i] != 0;
+                if (live[p]) sv[p] = state[(uint32_t)i];
+            }
+            for (uint32_t t = tid; t < T; t += NT) cnt[t] = lds_addr(cnt + t) << kHandleShift;
+            if (tid == 0) *any_flag = 0u;
+            __syncthreads();
+#pragma unroll
+            for (int p = 0; p < KPT; ++p) {
+                if (!live[p]) continue;
+                const nb::SplitState ss{sv[p].x, sv[p].y, sv[p].z, sv[p].w};
+                uint32_t r = ss.r;  // index J0; the later ones by split_step
+#pragma unroll
+                for (int j = J0; j < kR; ++j) {
+                    if (KX ? j < KX : j < (int)c.k) {
+                        if (j > J0) r = nb::split_step(r, ss, (uint32_t)j, c.fm.m);
+                        ridx[p][j] = r;
+                        rank[p][j] = atomicAdd(&cnt[__umulhi(r, tmul)], 4u);
+                    }
+                }
+            }
+            __syncthreads();
+            return;
+        }
         KeyBatch<FLAVOR, LAYOUT, KPT> kb;
         if (!STAGE) kb.load(keys, offsets, base + tid, NT, n);
         if (!STAGE) {  // (issued with the key loads: the gate bytes are read before the hash)
@@ -881,7 +925,7 @@ struct BinPhase1 {
         // block-local run, and index + rank stay in registers for phase 3; otherwise
         // only the index generator's start state (6 registers per key) is kept and
         // phase 3 regenerates the indices.
-        auto count_key = [&](int p, uint64_t h1, uint64_t h2) {
+        auto count_key = [&](int p, uint64_t h1, uint64_t h2, uint32_t key_id) {
             gen[p].start(h1, h2, c);
             IndexGen g = gen[p];
             if (KR > 0) {
@@ -894,6 +938,12 @@ struct BinPhase1 {
                             rank[p][j] = NB_DIAG_NOCOUNT ? g.r : atomicAdd(&cnt[__umulhi(g.r, tmul)], 4u);
                         }
                     }
+                }
+                if constexpr (ST == 1) {  // index KX and the wrap bit of every later step
+                    static_assert(KX > 0, "the state follows a fixed index range");
+                    g.next(c);
+                    const nb::SplitState ss = nb::split_state(g, c, (uint32_t)KX);
+                    state[key_id] = make_uint4(ss.r, ss.sb, ss.s2b, ss.bits);
                 }
             } else {
                 for (uint32_t j = 0; j < c.k; ++j) {
@@ -912,7 +962,7 @@ struct BinPhase1 {
                 kb.hash(c, keys, key_len, base + (uint64_t)p * NT + tid, p, &h1[p], &h2[p]);
 #pragma unroll
             for (int p = 0; p < KPT; ++p)
-                if (live[p]) count_key(p, h1[p], h2[p]);
+                if (live[p]) count_key(p, h1[p], h2[p], (uint32_t)(base + (uint64_t)p * NT + tid));
 #pragma unroll
             for (int p = 0; p < KPT; ++p) kid[p] = (uint32_t)(base + (uint64_t)p * NT + tid);
         } else {
@@ -1032,7 +1082,7 @@ struct BinPhase1 {
                     } else {
                         key_hashes_ptr<FLAVOR, LAYOUT == kFixedStride>(c, keys + b, len, &h1, &h2);
                     }
-                    count_key(p, h1, h2);
+                    count_key(p, h1, h2, kid[p]);
                 }
             }
         }
@@ -1537,12 +1587,14 @@ __host__ __device__ constexpr uint32_t probe_sort_offset_words(uint32_t T) {
 
 // Split probe (round 5): J0..J1 (J1 = 0: k) is the range of each key's indices this
 // launch bins; R2 marks the second round, which bins only the keys whose answer the
-// first round left at 1 and leaves the answers' initialisation to the first.
-template <int FLAVOR, int LAYOUT, bool STAGE, int KR, int J0 = 0, int J1 = 0, bool R2 = false>
+// first round left at 1 and leaves the answers' initialisation to the first.  ST (see
+// BinPhase1): the first round stores each key's index state, the second reads it
+// instead of the key.
+template <int FLAVOR, int LAYOUT, bool STAGE, int KR, int J0 = 0, int J1 = 0, bool R2 = false, int ST = 0>
 __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) void probe_bin_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
     uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc, uint64_t *__restrict__ buckets,
-    const uint64_t *__restrict__ words, uint8_t *__restrict__ out, ProbeGate gate) {
+    const uint64_t *__restrict__ words, uint8_t *__restrict__ out, ProbeGate gate, uint4 *state) {
     constexpr int NT = kProbeThreads;
     if (!gate_open(gate)) return;
     extern __shared__ uint32_t lds[];
@@ -1552,8 +1604,9 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
     uint32_t *sidx = lds + probe_sort_offset_words(T);  // [NT * k] indices, sorted by tile
     uint32_t *skid = sidx + NT * k;                     // [NT * k] their keys
     const uint64_t base = (uint64_t)blockIdx.x * NT;
-    BinPhase1<FLAVOR, LAYOUT, 1, NT, STAGE, KR, J1, J0, R2> ph;
+    BinPhase1<FLAVOR, LAYOUT, 1, NT, STAGE && ST != 2, KR, J1, J0, R2, ST> ph;
     if (R2) ph.gate = out;
+    ph.state = state;
     ph.run(keys, offsets, key_len, n, c, tc.mul, T, cnt, sidx, wave_sums + NT / 64 + 1, base);
     const bool valid = base + tid < n;  // (staged keys: the valid ones fill the first slots)
     if (!R2 && valid) out[ph.kid[0]] = 1;
@@ -1737,6 +1790,8 @@ struct Workspace {
     hipEvent_t ev_tile[2] = {nullptr, nullptr}, ev_start = nullptr;
     uint32_t *zeroed_alt = nullptr;
     size_t zeroed_alt_bytes = 0;
+    void *probe_state = nullptr;  // the split probe's index state between its rounds
+    size_t probe_state_bytes = 0;
     void *buckets_alt = nullptr;
     size_t bucket_alt_bytes = 0;
 };
@@ -2433,10 +2488,14 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
     if (bin_lds > kMaxBlockLds) return fail(NB_ERR_UNSUPPORTED, "tiled probe: LDS of the shape");
     const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
     auto bin = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR>;
-    auto bin1 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, kSplitJ, false>;
-    auto bin2 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, kSplitJ, 0, true>;
+    auto bin1 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, kSplitJ, false, 1>;
+    auto bin2 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, kSplitJ, 0, true, 2>;
     auto tile = probe_tile_kernel<kTileThreads>;
     split = split && c.k > (uint32_t)kSplitJ;
+    if (split && (size_t)chunk * 16 > ws->probe_state_bytes) {
+        NB_HIP(hipStreamSynchronize(st));  // (the old buffer may be in use on the stream)
+        if ((rc = grow(*ws, &ws->probe_state, &ws->probe_state_bytes, (size_t)chunk * 16))) return rc;
+    }
     if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(bin1, bin_lds)) || (rc = allow_lds(bin2, bin_lds)) ||
         (rc = allow_lds(tile, tile_lds)))
         return rc;
@@ -2449,7 +2508,8 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
         for (int round = 0; round < (split ? 2 : 1); ++round) {
             auto b = !split ? bin : round == 0 ? bin1 : bin2;
             hipLaunchKernelGGL(b, dim3((uint32_t)((cn + NT - 1) / NT)), dim3(NT), bin_lds, st, ck, co,
-                               key_len, cn, c, tc, sc, bk, words, out + done, gate);
+                               key_len, cn, c, tc, sc, bk, words, out + done, gate,
+                               split ? reinterpret_cast<uint4 *>(ws->probe_state) : nullptr);
             NB_HIP(hipGetLastError());
             hipLaunchKernelGGL(tile, dim3(tc.T), dim3(kTileThreads), tile_lds, st, tc, sc,
                                (const uint64_t *)bk, words, nwords, out + done, gate);
@@ -2474,6 +2534,10 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
                           probe_bin_lds_bytes(pT, c.k, !vec_layout(LAYOUT)) <= kMaxBlockLds;
     const ProbeGate none{nullptr, nullptr, 0, 0, 0};
     const uint32_t pct = (uint32_t)std::min<uint64_t>(knob(nb::kKnobProbeTiledPct), 101);
+    // the split path takes part in auto's choice for the k <= 8 tiled kernels (C3 / C4's
+    // filters: k = 7); on C5's shape (32-byte keys, k = 10) it lost at every mix
+    const uint32_t split_pct = c.k <= 8 && c.k > (uint32_t)kSplitJ
+                                   ? (uint32_t)std::min<uint64_t>(knob(nb::kKnobProbeSplitPct), 101) : 101u;
     if (path == 1 || !tiled_ok || (path == 0 && n < kProbeTiledMin))
         return launch_probe_lane<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, out, st, none);
     auto tiled = [&](const uint8_t *k_, const uint64_t *o_, uint64_t n_, uint8_t *out_,
@@ -2526,14 +2590,18 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         volatile uint32_t *hs = ws->probe_hits_host;
         uint64_t h = 0;
         for (uint32_t b = 0; b < kProbeSampleBlocks; ++b) h += hs[b];
-        if (probe_pick_tiled(h, S, pct)) return tiled(rk, ro, n - S, out + S, none);  // as gate_open decides
+        const uint32_t pick = probe_pick(h, S, pct, split_pct);  // as gate_open decides
+        if (pick != 1) return tiled(rk, ro, n - S, out + S, none, pick == 3);
         return launch_probe_lane<FLAVOR, LAYOUT>(rk, ro, key_len, n - S, c, words, out + S, st, none);
     }
-    const ProbeGate lane{nullptr, ws->probe_hits, kProbeSampleBlocks, (uint32_t)S, 1, pct};
-    const ProbeGate tile{nullptr, ws->probe_hits, kProbeSampleBlocks, (uint32_t)S, 2, pct};
+    const ProbeGate lane{nullptr, ws->probe_hits, kProbeSampleBlocks, (uint32_t)S, 1, pct, split_pct};
+    const ProbeGate tile{nullptr, ws->probe_hits, kProbeSampleBlocks, (uint32_t)S, 2, pct, split_pct};
+    const ProbeGate splt{nullptr, ws->probe_hits, kProbeSampleBlocks, (uint32_t)S, 3, pct, split_pct};
     if ((rc = launch_probe_lane<FLAVOR, LAYOUT>(rk, ro, key_len, n - S, c, words, out + S, st, lane)))
         return rc;
-    return tiled(rk, ro, n - S, out + S, tile);
+    if ((rc = tiled(rk, ro, n - S, out + S, tile))) return rc;
+    if (split_pct <= 100) return tiled(rk, ro, n - S, out + S, splt, true);
+    return NB_OK;
 }
 
 template <int FLAVOR>
@@ -2699,6 +2767,7 @@ int nb_shutdown(void) {
                 if (e) (void)hipEventDestroy(e);
             if (w->zeroed_alt) (void)hipFree(w->zeroed_alt);
             if (w->buckets_alt) (void)hipFree(w->buckets_alt);
+            if (w->probe_state) (void)hipFree(w->probe_state);
             if (w->probe_hits) (void)hipFree(w->probe_hits);
             if (w->probe_hits_host) (void)hipHostFree(w->probe_hits_host);
             if (w->ev_probe) (void)hipEventDestroy(w->ev_probe);

@@ -143,3 +143,26 @@ def test_probe_32byte_keys_large_k_full_filter(dev, oracle, knobs, path, k):
     want = oracle.probe(0, buf, None, 32, n, m, k, SEED, words)
     np.testing.assert_array_equal(got, want)
     assert got[:npres].all()
+
+
+@pytest.mark.parametrize("split_pct", ["13", "101"])
+@pytest.mark.parametrize("pc", [5, 30, 70])
+def test_auto_mixed_batches(dev, oracle, knobs, probe_shapes, pc, split_pct):
+    """Auto on batches whose sample sees pc % present keys (every key i with
+    i % 20 < pc / 5 present): lane, split (NB_PROBE_SPLIT_PCT 13: 13-50 %) or tiled,
+    bit-exact against the oracle whichever it picks; NB_PROBE_SPLIT_PCT=101 leaves
+    the two-way choice."""
+    from nasp_bloom import synth
+    buf, offs, kl, n, m, k, fl = probe_shapes["c4_fixed16"]
+    knobs(NB_PROBE_PATH="auto", NB_PROBE_SPLIT_PCT=split_pct)
+    npres = n // 2
+    words = device_words(dev, buf, None, kl, npres, m, k, fl)
+    absent = synth.fixed_keys(n, kl, seed=77)
+    mixed = absent.copy()
+    idx = np.nonzero(np.arange(n) % 20 < pc // 5)[0]
+    mv, bv = mixed[: n * kl].reshape(n, kl), buf[: n * kl].reshape(n, kl)
+    mv[idx] = bv[idx % npres]
+    got = dev_probe(dev, mixed, None, kl, n, m, k, SEED, words, fl)
+    want = oracle.probe(fl, mixed, None, kl, n, m, k, SEED, words)
+    np.testing.assert_array_equal(got, want)
+    assert got[idx].all()

@@ -91,15 +91,15 @@ def main():
             nbm.probe_device(b, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out, stream=st)
             torch.cuda.synchronize(dev)
             ref[name] = out.clone()
-    variants = ([] if args.no_lane else [("lane", "lane", 0, "30")]) + [
-        (f"tiled C={c / 1e6 if c else 'policy'}M", "tiled", c, "30") for c in map(int, args.chunks.split(",") if args.chunks else [])
-    ] + ([("split", "split", 0, "30")] if args.split else []) + [
-        (f"auto pct={p}", "auto", 0, p) for p in filter(None, args.auto_pct.split(","))]
+    variants = ([] if args.no_lane else [("lane", "lane", 0, "30", {})]) + [
+        (f"tiled C={c / 1e6 if c else 'policy'}M", "tiled", c, "30", {}) for c in map(int, args.chunks.split(",") if args.chunks else [])
+    ] + ([("split", "split", 0, "30", {})] if args.split else []) + [
+        (f"auto pct={p}", "auto", 0, p, {}) for p in filter(None, args.auto_pct.split(","))]
     table = {}
     bad = 0
     for rep in range(reps):
-        for label, path, chunk, pct in variants:
-            with nbm.knobs(NB_PROBE_PATH=path, NB_PROBE_CHUNK=str(chunk), NB_PROBE_TILED_PCT=pct):
+        for label, path, chunk, pct, extra in variants:
+            with nbm.knobs(NB_PROBE_PATH=path, NB_PROBE_CHUNK=str(chunk), NB_PROBE_TILED_PCT=pct, **extra):
                 for name, b in batches.items():
                     nbm.probe_device(b, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out, stream=st)
                     torch.cuda.synchronize(dev)
@@ -116,7 +116,7 @@ def main():
                     print(f"rep {rep} {label:>16} {name:>8} {ms:8.3f} ms  {wl.n / ms / 1e6:7.2f} Gkeys/s",
                           flush=True)
     print(f"summary (ms per {wl.n / 1e6:.0f}M-key call, wall clock over 5 calls; min over reps):")
-    for label, _, _, _ in variants:
+    for label, _, _, _, _ in variants:
         print(f"  {label:>16} " + "  ".join(f"{n} {min(table[(label, n)]):7.3f}" for n in batches))
     print(f"answers identical to the lane path: {'yes' if bad == 0 else f'NO ({bad} mismatches)'}")
     return 1 if bad else 0
