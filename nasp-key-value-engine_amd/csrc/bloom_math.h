@@ -275,27 +275,6 @@ struct IndexGen {
     }
 };
 
-// The split tiled probe's hand-over between its two rounds (bloom_kernels.hip,
-// BinPhase1 ST = 1 / 2): a key's generator at index j0 as four words -- the index,
-// the two biased step sizes and the wrap bit of every later step (bit j: the step to
-// index j wraps x) -- from which its later indices follow without h1, h2 or x.
-struct SplitState {
-    uint32_t r, sb, s2b, bits;
-};
-NB_HD SplitState split_state(const IndexGen &g, const FilterConsts &c, uint32_t j0) {  // g at index j0
-    SplitState s{g.r, g.sb, g.s2b, 0u};
-    uint64_t x = g.x;
-    for (uint32_t j = j0 + 1; j < c.k; ++j) {
-        const uint64_t nx = x + g.h2;
-        s.bits |= (nx < x ? 1u : 0u) << j;
-        x = nx;
-    }
-    return s;
-}
-NB_HD uint32_t split_step(uint32_t r, const SplitState &s, uint32_t j, uint32_t m) {  // index j-1 -> j
-    const uint32_t t = r + (((s.bits >> j) & 1u) ? s.s2b : s.sb);
-    return t < r ? t : t + m;  // as IndexGen::next
-}
 
 // ------------------------------------------------- word-stream hashing ----
 // Both hashes of one key computed from its bytes viewed as 8-byte little-endian

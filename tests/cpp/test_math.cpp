@@ -51,23 +51,6 @@ int main() {
                 if (i) g.next(c);
                 if (g.r != (uint32_t)((h1 + (uint64_t)i * h2) % m)) ++bad;
             }
-            // the split probe's hand-over at index j0 (split_state / split_step): the
-            // later indices from four words, for every j0 the rounds could split at
-            for (uint32_t kk : {3u, 7u, 10u, 16u, 32u}) {
-                nb::FilterConsts ck = c;
-                ck.k = kk;
-                for (uint32_t j0 = 1; j0 < kk; j0 += (kk > 8 ? 5 : 1)) {
-                    nb::IndexGen s;
-                    s.start(h1, h2, ck);
-                    for (uint32_t i = 1; i <= j0; ++i) s.next(ck);
-                    const nb::SplitState st = nb::split_state(s, ck, j0);
-                    uint32_t r = st.r;
-                    for (uint32_t i = j0; i < kk; ++i) {
-                        if (i > j0) r = nb::split_step(r, st, i, m);
-                        if (r != (uint32_t)((h1 + (uint64_t)i * h2) % m)) ++bad;
-                    }
-                }
-            }
         }
         // modular add of the index step, including sums that carry out of 32 bits
         for (int t = 0; t < 2000; ++t) {
