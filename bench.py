@@ -208,9 +208,12 @@ def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=
     just built: the batch's own keys (every one present) and as many absent keys
     (their positive rate is the filter's measured false-positive rate), on each
     probe path (NB_PROBE_PATH): `auto` (the library's default: a sampled prefix picks
-    the path on the device), `lane` (one lane per key, k gathers with early exit) and
-    `tiled` (lookups binned by filter tile and tested in LDS).  Reported beside
-    `value`."""
+    the path on the device), `lane` (one lane per key, k gathers with early exit),
+    `tiled` (lookups binned by filter tile and tested in LDS) and `split` (the tiled
+    path in two rounds: two indices of every key, then the rest of the keys still
+    present).  Fixed-length keys also get a mixed batch, `p30`: 3 of every 10 keys
+    present, the rest absent (LSM point lookups over one level's SSTables are mostly
+    misses).  Reported beside `value`."""
     import torch
     import nasp_bloom as nbm
     from nasp_bloom import synth
@@ -218,11 +221,17 @@ def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=
     absent = torch.from_numpy(a_np).to(dev)
     a_o = torch.from_numpy(a_offs.view(np.int64)).to(dev) if a_offs is not None else None
     out_t = torch.empty(wl.n, dtype=torch.uint8, device=dev)
+    batches = [("present", keys, offs), ("absent", absent, a_o)]
+    if offs is None and a_o is None and wl.n % 10 == 0 and keys.numel() == wl.n * key_len:
+        mixed = absent.clone()
+        mv, kv = mixed.view(wl.n // 10, 10, key_len), keys.view(wl.n // 10, 10, key_len)
+        mv[:, :3] = kv[:, :3]
+        batches.append(("p30", mixed, None))
     res = {}
-    for path in ("auto", "lane", "tiled"):
+    for path in ("auto", "lane", "tiled", "split"):
         r = {}
         with nbm.knobs(NB_PROBE_PATH=path):
-            for name, kk, oo in (("present", keys, offs), ("absent", absent, a_o)):
+            for name, kk, oo in batches:
                 with torch.cuda.stream(stream):
                     nbm.probe_device(kk, oo, key_len, wl.n, wl.m, wl.k, seed, flavor, words, out_t,
                                      stream=stream)
@@ -240,9 +249,10 @@ def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=
                 r[name] = {"value": round(wl.n / (ms * 1e-3) / 1e6, 3), "unit": "Mkeys/s",
                            "ms": round(ms, 4), "positive_rate": round(float(out_t.float().mean()), 6)}
         res[path] = r
-    res["note"] = ("auto = the default (lane kernel on a 4 096-key sample, its hit rate picks lane "
-                   "or tiled for the rest); absent keys from another seed; ms = wall clock per call "
-                   "over 5 back-to-back calls between device synchronisations")
+    res["note"] = ("auto = the default (lane kernel on a 4 096-key sample, its hit rate picks lane, "
+                   "split or tiled for the rest); absent keys from another seed; p30 = keys 0-2 of "
+                   "every 10 present, the rest absent; ms = wall clock per call over 5 back-to-back "
+                   "calls between device synchronisations")
     return res
 
 

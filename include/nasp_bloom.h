@@ -79,10 +79,12 @@ uint64_t nb_device_merkle_count(void);
  * environment variable of the same name once, on first use; nb_set_knob changes
  * it for the whole process afterwards (thread-safe).  Names: NB_BUILD_PATH
  * (0 auto, 1 atomic, 2 tiled), NB_PROBE_PATH (0 auto, 1 one lane per key, 2 tiled,
- * 3 split: the tiled probe in two rounds), NB_PROBE_SPLIT_PCT (auto, k <= 8: the split
- * path from this percentage of present keys in its sample up to 50, default 13),
+ * 3 split: the tiled probe in two rounds), NB_PROBE_SPLIT_PCT (auto, k > 2: the split
+ * path from this percentage of present keys in its sample up to 65, 55 for k > 8;
+ * default 0, the policy: 7 for k <= 8, 18 above; > 100: never),
  * NB_PROBE_CHUNK (keys per tiled-probe pass; 0: the policy), NB_PROBE_TILED_PCT (auto's
- * tiled path from this percentage of present keys in its sample, default 30),
+ * tiled path from this percentage of present keys in its sample when it never splits,
+ * default 30),
  * NB_PACK, NB_TILE_BITS, NB_SHARDS, NB_CHUNK_KEYS, NB_TWO_LEVEL, NB_PACK5,
  * NB_ENTRY32, NB_RANK, NB_FIXED32, NB_FPMOD, NB_KEXACT, NB_BIN_WIDE, NB_OVERLAP (two-level
  * sub-passes pipelined over a second stream of the workspace: 0 off, 1/2 normal/high
@@ -222,15 +224,16 @@ int nb_build_device_ex(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_
 /* Batch probe, device-resident.  Large batches (>= 4M keys) of 16-, 32-byte or
  * variable-length keys with k <= 8 (k <= 16 for 32-byte keys) may take the tiled
  * path (lookups binned by filter tile and tested in LDS: ~4x the one-lane-per-key
- * rate for present keys, ~half of it for absent ones) or, for k <= 8, the split tiled
+ * rate for present keys, ~half of it for absent ones) or, for k > 2, the split tiled
  * path (two rounds: every key's first two indices, then the rest for the keys still
  * possibly present); NB_PROBE_PATH=0 (auto) probes the first 4 096 keys one lane per
- * key and picks from the share of them present: for k <= 8 the lane path below
- * NB_PROBE_SPLIT_PCT (13 %), the split path up to 50 %, the tiled path from there;
- * otherwise the tiled path from NB_PROBE_TILED_PCT (30 %).  Auto waits once for that
- * sample (its 16 counts land in host-mapped memory) -- except while the stream is
- * being captured into a graph, where every path is launched and gated on the sample on
- * the device.  Same answers on every path. */
+ * key and picks from the share of them present: the lane path below NB_PROBE_SPLIT_PCT
+ * (the policy: 7 % for k <= 8, 18 % above), the split path up to 65 % (55 % for
+ * k > 8), the tiled path from there (NB_PROBE_SPLIT_PCT > 100: the tiled path from
+ * NB_PROBE_TILED_PCT, 30 %).  Auto waits once for that sample (its 16 counts land in
+ * host-mapped memory) -- except while the stream is being captured into a graph, where
+ * every path is launched and gated on the sample on the device.  Same answers on every
+ * path. */
 int nb_probe_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
                     uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
                     const uint64_t *d_words, uint8_t *d_out, void *stream);

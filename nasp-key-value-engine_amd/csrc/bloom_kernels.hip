@@ -255,25 +255,27 @@ struct ProbeGate {
     uint32_t blocks;         // sample blocks (words of decide)
     uint32_t sample;         // keys in the sample
     uint32_t want;           // 1 the lane path, 2 the tiled path, 3 the split tiled path
-    uint32_t pct = 30;       // tiled from this percentage of the sample present on
+    uint32_t pct = 30;       // the tiled path from this percentage of the sample present
     uint32_t split_pct = 101;  // the split path from this percentage (> 100: never) up
-                               // to kSplitTiledPct, where the tiled path takes over
+                               // to pct, where the tiled path takes over
 };
-// Where the split path hands over to the one-round tiled path (on C4's
-// filter the two cross at ~50 % present, profiles/r05_probe_split_c4.txt)
-constexpr uint32_t kSplitTiledPct = 50;
+// Auto's thresholds with the split path, per shape (the crossings of
+// profiles/r05_probe_split_final_{c4,c5shape}.txt): lane -> split at ~6 % present on
+// C4's filter (16-byte keys, k = 7) and ~18 % on C5's shape (32-byte keys, k = 10: the
+// lane kernel's absent keys are cheap there) -- NB_PROBE_SPLIT_PCT 0, the policy --
+// and split -> tiled at ~67 % / ~55 %.
+constexpr uint32_t split_pct_policy(uint32_t k) { return k <= 8 ? 7u : 18u; }
+constexpr uint32_t split_tiled_pct(uint32_t k) { return k <= 8 ? 65u : 55u; }
 // Auto's choice from the sample's hit count h of s keys: 1 lane, 2 tiled, 3 split.
 // Without the split path: tiled when at least pct % were present (a present key costs
 // the lane kernel ~k gathers, an absent one ~2, and the tiled path a fixed pass plus
 // ~k/2 miss stores per absent key; on C3 / C4's filter and on C5's shape the two break
-// even at ~30 % present).  With it (k <= 8): lane below split_pct %, split up to
-// kSplitTiledPct %, tiled from there.
+// even at ~30 % present).  With it: lane below split_pct %, split below pct %, tiled
+// from there.
 __host__ __device__ inline uint32_t probe_pick(uint64_t h, uint64_t s, uint32_t pct, uint32_t split_pct) {
-    if (split_pct <= 100) {
-        if (100 * h < (uint64_t)split_pct * s) return 1u;
-        return 100 * h < (uint64_t)kSplitTiledPct * s ? 3u : 2u;
-    }
-    return 100 * h >= (uint64_t)pct * s ? 2u : 1u;
+    if (100 * h >= (uint64_t)pct * s) return 2u;
+    if (split_pct <= 100 && 100 * h >= (uint64_t)split_pct * s) return 3u;
+    return 1u;
 }
 __device__ __forceinline__ bool gate_open(const ProbeGate &g) {
     if (!g.decide) return true;
@@ -848,23 +850,23 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
 // The split tiled probe (round 5) counts a range of each key's indices: J0 is the
 // first one counted (the earlier ones only advance the generator; KX, when set, is
 // the end), and with GATE a key is counted only while gate[kid] != 0 (its answer
-// after the first round); live[p] says whether slot p was counted.  ST = 1: the first
-// round also stores each key's index state after its KX indices (state[kid] = {next
-// index, the two biased step sizes, the wrap bit of every later step}); ST = 2: the
-// second round reads that state instead of loading and hashing the key.
+// after the first round); live[p] says whether slot p was counted.  With IDS
+// (register-loaded keys only) the launch's keys are ids[0, n): the second round over
+// the compacted list of the keys the first left at 1 (probe_compact_kernel).
 template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR, int KX = 0, int J0 = 0,
-          bool GATE = false, int ST = 0>
+          bool GATE = false, bool IDS = false>
 struct BinPhase1 {
     static constexpr int kR = KR > 0 ? KR : 1;
-    static_assert(KR == 0 || (uint64_t)KPT * NT * KR < (1u << (kHandleShift - 2)),
+    static_assert(KR == 0 || (uint64_t)KPT * NT * (KX ? KX - J0 : KR) < (1u << (kHandleShift - 2)),
                   "a block's ranks must fit the placement handle's low bits");
     static_assert(J0 == 0 || KR > 0, "an index range needs the rank registers");
+    static_assert(!IDS || !STAGE, "a key list needs register-loaded keys");
     IndexGen gen[KPT];
     uint32_t ridx[KPT][kR], rank[KPT][kR];
     uint32_t kid[KPT];  // (mod 2^32: the probe launches chunks of < 2^32 keys)
     bool live[KPT];
     const uint8_t *gate = nullptr;
-    uint4 *state = nullptr;  // ST > 0: [keys of the launch] index state between the rounds
+    const uint32_t *ids = nullptr;  // IDS: the keys of the launch
 
     __device__ __forceinline__ void run(const uint8_t *__restrict__ keys,
                                         const uint64_t *__restrict__ offsets, uint32_t key_len,
@@ -872,39 +874,18 @@ struct BinPhase1 {
                                         uint32_t *cnt, uint32_t *sorted, uint32_t *any_flag,
                                         uint64_t base) {
         const uint32_t tid = threadIdx.x;
-        if constexpr (ST == 2) {  // the second round: no key loads, no hash
-            static_assert(KR > 0 && GATE, "the state round counts gated index ranges");
-            uint4 sv[KPT];
-#pragma unroll
-            for (int p = 0; p < KPT; ++p) {
-                const uint64_t i = base + (uint64_t)p * NT + tid;
-                kid[p] = (uint32_t)i;
-                live[p] = i < n && gate[(uint32_t)i] != 0;
-                if (live[p]) sv[p] = state[(uint32_t)i];
-            }
-            for (uint32_t t = tid; t < T; t += NT) cnt[t] = lds_addr(cnt + t) << kHandleShift;
-            if (tid == 0) *any_flag = 0u;
-            __syncthreads();
-#pragma unroll
-            for (int p = 0; p < KPT; ++p) {
-                if (!live[p]) continue;
-                const nb::SplitState ss{sv[p].x, sv[p].y, sv[p].z, sv[p].w};
-                uint32_t r = ss.r;  // index J0; the later ones by split_step
-#pragma unroll
-                for (int j = J0; j < kR; ++j) {
-                    if (KX ? j < KX : j < (int)c.k) {
-                        if (j > J0) r = nb::split_step(r, ss, (uint32_t)j, c.fm.m);
-                        ridx[p][j] = r;
-                        rank[p][j] = atomicAdd(&cnt[__umulhi(r, tmul)], 4u);
-                    }
-                }
-            }
-            __syncthreads();
-            return;
-        }
         KeyBatch<FLAVOR, LAYOUT, KPT> kb;
-        if (!STAGE) kb.load(keys, offsets, base + tid, NT, n);
-        if (!STAGE) {  // (issued with the key loads: the gate bytes are read before the hash)
+        if (IDS) {
+#pragma unroll
+            for (int p = 0; p < KPT; ++p) {
+                const uint64_t j = base + (uint64_t)p * NT + tid;
+                live[p] = j < n;
+                kid[p] = live[p] ? ids[(uint32_t)j] : 0u;
+                kb.load_one(p, keys, offsets, kid[p], live[p] ? ~0ull : 0ull);
+            }
+        } else if (!STAGE) {
+            kb.load(keys, offsets, base + tid, NT, n);
+            // (issued with the key loads: the gate bytes are read before the hash)
 #pragma unroll
             for (int p = 0; p < KPT; ++p) {
                 const uint64_t i = base + (uint64_t)p * NT + tid;
@@ -925,7 +906,7 @@ struct BinPhase1 {
         // block-local run, and index + rank stay in registers for phase 3; otherwise
         // only the index generator's start state (6 registers per key) is kept and
         // phase 3 regenerates the indices.
-        auto count_key = [&](int p, uint64_t h1, uint64_t h2, uint32_t key_id) {
+        auto count_key = [&](int p, uint64_t h1, uint64_t h2) {
             gen[p].start(h1, h2, c);
             IndexGen g = gen[p];
             if (KR > 0) {
@@ -938,12 +919,6 @@ struct BinPhase1 {
                             rank[p][j] = NB_DIAG_NOCOUNT ? g.r : atomicAdd(&cnt[__umulhi(g.r, tmul)], 4u);
                         }
                     }
-                }
-                if constexpr (ST == 1) {  // index KX and the wrap bit of every later step
-                    static_assert(KX > 0, "the state follows a fixed index range");
-                    g.next(c);
-                    const nb::SplitState ss = nb::split_state(g, c, (uint32_t)KX);
-                    state[key_id] = make_uint4(ss.r, ss.sb, ss.s2b, ss.bits);
                 }
             } else {
                 for (uint32_t j = 0; j < c.k; ++j) {
@@ -962,9 +937,10 @@ struct BinPhase1 {
                 kb.hash(c, keys, key_len, base + (uint64_t)p * NT + tid, p, &h1[p], &h2[p]);
 #pragma unroll
             for (int p = 0; p < KPT; ++p)
-                if (live[p]) count_key(p, h1[p], h2[p], (uint32_t)(base + (uint64_t)p * NT + tid));
+                if (live[p]) count_key(p, h1[p], h2[p]);
+            if (!IDS)
 #pragma unroll
-            for (int p = 0; p < KPT; ++p) kid[p] = (uint32_t)(base + (uint64_t)p * NT + tid);
+                for (int p = 0; p < KPT; ++p) kid[p] = (uint32_t)(base + (uint64_t)p * NT + tid);
         } else {
             // Variable-length (or odd fixed-length) keys, one sub-batch of NT keys at a
             // time: its keys are one contiguous byte range.  When that fits the stage
@@ -1082,7 +1058,7 @@ struct BinPhase1 {
                     } else {
                         key_hashes_ptr<FLAVOR, LAYOUT == kFixedStride>(c, keys + b, len, &h1, &h2);
                     }
-                    count_key(p, h1, h2, kid[p]);
+                    count_key(p, h1, h2);
                 }
             }
         }
@@ -1587,29 +1563,43 @@ __host__ __device__ constexpr uint32_t probe_sort_offset_words(uint32_t T) {
 
 // Split probe (round 5): J0..J1 (J1 = 0: k) is the range of each key's indices this
 // launch bins; R2 marks the second round, which bins only the keys whose answer the
-// first round left at 1 and leaves the answers' initialisation to the first.  ST (see
-// BinPhase1): the first round stores each key's index state, the second reads it
-// instead of the key.
-template <int FLAVOR, int LAYOUT, bool STAGE, int KR, int J0 = 0, int J1 = 0, bool R2 = false, int ST = 0>
+// first round left at 1 and leaves the answers' initialisation to the first.  PKPT
+// keys per thread: the first round bins two indices per key, so it takes four keys
+// per thread (runs four times as long, a quarter of the reservations) in the LDS the
+// one-round kernel's k indices of one key take.  IDS (the second round, register-loaded
+// keys): the keys are the compacted list ids[0, *nlive) of the first round's survivors
+// (probe_compact_kernel), so the hash and the runs go to live keys only; the grid is
+// sized for every key of the pass and the blocks past the list return at once.
+template <int FLAVOR, int LAYOUT, bool STAGE, int KR, int J0 = 0, int J1 = 0, bool R2 = false, int PKPT = 1,
+          bool IDS = false>
 __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) void probe_bin_kernel(
     const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
     uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc, uint64_t *__restrict__ buckets,
-    const uint64_t *__restrict__ words, uint8_t *__restrict__ out, ProbeGate gate, uint4 *state) {
+    const uint64_t *__restrict__ words, uint8_t *__restrict__ out, ProbeGate gate,
+    const uint32_t *__restrict__ ids, const uint32_t *__restrict__ nlive) {
     constexpr int NT = kProbeThreads;
     if (!gate_open(gate)) return;
+    if (IDS) {
+        n = *nlive;  // block-uniform
+        if ((uint64_t)blockIdx.x * (NT * PKPT) >= n) return;
+    }
     extern __shared__ uint32_t lds[];
     const uint32_t T = tc.T, tid = threadIdx.x, k = c.k;
     uint32_t *cnt = lds, *S = lds + T, *GX = lds + 2 * T, *L = lds + 3 * T;
     uint32_t *wave_sums = lds + 4 * T;  // [NT/64 + 2]
-    uint32_t *sidx = lds + probe_sort_offset_words(T);  // [NT * k] indices, sorted by tile
-    uint32_t *skid = sidx + NT * k;                     // [NT * k] their keys
-    const uint64_t base = (uint64_t)blockIdx.x * NT;
-    BinPhase1<FLAVOR, LAYOUT, 1, NT, STAGE && ST != 2, KR, J1, J0, R2, ST> ph;
+    const uint32_t keff = PKPT * ((J1 ? (uint32_t)J1 : k) - J0);  // (probe_keff on the host)
+    uint32_t *sidx = lds + probe_sort_offset_words(T);  // [NT * keff] indices, sorted by tile
+    uint32_t *skid = sidx + NT * keff;                  // [NT * keff] their keys
+    const uint64_t base = (uint64_t)blockIdx.x * (NT * PKPT);
+    BinPhase1<FLAVOR, LAYOUT, PKPT, NT, STAGE, KR, J1, J0, R2, IDS> ph;
     if (R2) ph.gate = out;
-    ph.state = state;
+    ph.ids = ids;
     ph.run(keys, offsets, key_len, n, c, tc.mul, T, cnt, sidx, wave_sums + NT / 64 + 1, base);
-    const bool valid = base + tid < n;  // (staged keys: the valid ones fill the first slots)
-    if (!R2 && valid) out[ph.kid[0]] = 1;
+    if (!R2) {
+#pragma unroll
+        for (int p = 0; p < PKPT; ++p)  // (staged keys: the valid ones fill the first slots)
+            if (base + (uint64_t)p * NT + tid < n) out[ph.kid[p]] = 1;
+    }
     // counts from the placement handles (A_t << kHandleShift | 4 rank, see BinPhase1)
     for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << kHandleShift)) >> 2;
     __syncthreads();
@@ -1624,14 +1614,17 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
         L[t] = S[t] + (g < tc.cap ? tc.cap - g : 0u);
     }
     // placement (the reservations' round trips overlap it)
-    if (ph.live[0]) {
 #pragma unroll
-        for (int j = J0; j < KR; ++j)
-            if (J1 ? j < J1 : j < (int)k) {
-                const uint32_t pos = S[ph.ridx[0][j] >> tc.ts] + ((ph.rank[0][j] & kHandleMask) >> 2);
-                sidx[pos] = ph.ridx[0][j];
-                skid[pos] = ph.kid[0];
-            }
+    for (int p = 0; p < PKPT; ++p) {
+        if (ph.live[p]) {
+#pragma unroll
+            for (int j = J0; j < KR; ++j)
+                if (J1 ? j < J1 : j < (int)k) {
+                    const uint32_t pos = S[ph.ridx[p][j] >> tc.ts] + ((ph.rank[p][j] & kHandleMask) >> 2);
+                    sidx[pos] = ph.ridx[p][j];
+                    skid[pos] = ph.kid[p];
+                }
+        }
     }
     __syncthreads();
     // write-out: one 64-bit entry per index, runs contiguous; an entry past its
@@ -1645,6 +1638,64 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
             out[kq] = 0;
         }
     }
+}
+
+// The split probe's survivors of its first round: ids (in the pass) of the keys whose
+// answer is still 1, appended to ids[] (block order arbitrary, in key order within a
+// block) and counted in *nlive (zeroed before the launch).  16 answers per thread (four
+// 4-byte loads when the answers are 4-byte aligned), one reservation atomic per block
+// of 16 384 keys: the blocks' atomics all hit *nlive, which serialises them (~10 ns
+// each; four answers per thread took 0.15 ms per 50M-key pass on them alone).  The
+// block's ids are staged in LDS (dynamic, kCompactLds) and copied out coalesced: a
+// lane's own 16 stores would each hit a different line.
+constexpr int kCompactThreads = 1024, kCompactPer = 16;
+constexpr size_t kCompactLds = ((size_t)kCompactThreads * kCompactPer + kCompactThreads / 64 + 2) * 4;
+__global__ __launch_bounds__(kCompactThreads) void probe_compact_kernel(const uint8_t *__restrict__ ans,
+                                                                         uint32_t n, uint32_t *__restrict__ ids,
+                                                                         uint32_t *__restrict__ nlive,
+                                                                         ProbeGate gate) {
+    if (!gate_open(gate)) return;
+    extern __shared__ uint32_t stage[];  // [NT * 16] the block's ids, then the wave sums
+    uint32_t *wsum = stage + kCompactThreads * kCompactPer;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t i0 = (blockIdx.x * kCompactThreads + tid) * kCompactPer;
+    uint32_t live = 0;
+    if ((reinterpret_cast<uintptr_t>(ans) & 3) == 0 && i0 + kCompactPer <= n) {  // (kernel-uniform alignment)
+        const uint32_t *a4 = reinterpret_cast<const uint32_t *>(ans + i0);
+#pragma unroll
+        for (int w = 0; w < kCompactPer / 4; ++w) {
+            const uint32_t v = a4[w];
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                if ((v >> (8 * b)) & 0xffu) live |= 1u << (4 * w + b);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < kCompactPer; ++q)
+            if (i0 + q < n && ans[i0 + q]) live |= 1u << q;
+    }
+    const uint32_t cnt = __popc(live), incl = wave_inclusive_scan(cnt);
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    if (wid == 0) {
+        constexpr uint32_t kW = kCompactThreads / 64;
+        const uint32_t w = lane < kW ? wsum[lane] : 0u, wi = wave_inclusive_scan(w);
+        if (lane < kW) wsum[lane] = wi - w;
+        if (lane == kW - 1) {
+            wsum[kW] = wi;
+            wsum[kW + 1] = wi ? atomicAdd(nlive, wi) : 0u;
+        }
+    }
+    __syncthreads();
+    uint32_t o = wsum[wid] + incl - cnt;  // in the block
+    while (live) {
+        const uint32_t q = __builtin_ctz(live);
+        live &= live - 1;
+        stage[o++] = i0 + q;
+    }
+    __syncthreads();
+    const uint32_t total = wsum[kCompactThreads / 64], gb = wsum[kCompactThreads / 64 + 1];
+    for (uint32_t j = tid; j < total; j += kCompactThreads) ids[gb + j] = stage[j];
 }
 
 template <int NT = kTileThreads>
@@ -1790,8 +1841,6 @@ struct Workspace {
     hipEvent_t ev_tile[2] = {nullptr, nullptr}, ev_start = nullptr;
     uint32_t *zeroed_alt = nullptr;
     size_t zeroed_alt_bytes = 0;
-    void *probe_state = nullptr;  // the split probe's index state between its rounds
-    size_t probe_state_bytes = 0;
     void *buckets_alt = nullptr;
     size_t bucket_alt_bytes = 0;
 };
@@ -2434,8 +2483,9 @@ TileCfg probe_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
 // one workgroup's 160 KiB: 32-byte keys at k = 12..16 over 4 096 tiles do not
 // (163 968 B at k = 12), and those batches take the lane path.
 constexpr size_t kMaxBlockLds = 160 * 1024;
-size_t probe_bin_lds_bytes(uint32_t T, uint32_t k, bool stage) {
-    size_t sort_bytes = (size_t)2 * kProbeThreads * k * 4;
+// keff = entries a thread bins: k for the one-round kernel (probe_keff for a round)
+size_t probe_bin_lds_bytes(uint32_t T, uint32_t keff, bool stage) {
+    size_t sort_bytes = (size_t)2 * kProbeThreads * keff * 4;
     if (stage) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(kProbeThreads));
     return (size_t)probe_sort_offset_words(T) * 4 + sort_bytes;
 }
@@ -2459,6 +2509,11 @@ int launch_probe_lane(const uint8_t *keys, const uint64_t *offsets, uint32_t key
 
 // The split tiled probe's first round: each key's first kSplitJ indices.
 constexpr int kSplitJ = 2;
+constexpr int kSplitKPT = 4;  // keys per thread of the split path's first round
+// entries per thread of a probe_bin_kernel launch (its keff)
+constexpr uint32_t probe_keff(uint32_t k, int j0, int j1, int pkpt) {
+    return (uint32_t)pkpt * ((j1 ? (uint32_t)j1 : k) - (uint32_t)j0);
+}
 
 // split: two rounds per pass -- the first bins every key's first kSplitJ indices and
 // answers the keys with a zero among them, the second bins the other k - kSplitJ
@@ -2483,21 +2538,30 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
     const uint64_t passes = (n + budget - 1) / budget;
     const uint64_t chunk = std::max<uint64_t>(1, (n + passes - 1) / passes);
     const TileCfg tc = probe_tiles(c.fm.m, chunk, c.k);
-    if ((rc = ws_reserve(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * 8, &sc))) return rc;
+    // register-loaded keys: the split path's second round runs over the compacted list
+    // of the first round's survivors -- a count word, then the ids -- kept in the
+    // workspace's second bucket array (the two-level build's; unused by the probe) and
+    // reserved on every tiled probe of such a shape, so that a warm-up on the one-round
+    // path sizes it for a later capture of auto's gated paths
+    const bool compact = !STAGE && c.k > (uint32_t)kSplitJ;
+    const size_t ids_bytes = compact ? (chunk + 16) * 4 : 0;
+    if ((rc = ws_reserve(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * 8, &sc, ids_bytes))) return rc;
+    uint32_t *nlive = compact ? reinterpret_cast<uint32_t *>(ws->buckets2) : nullptr;
+    uint32_t *ids = compact ? nlive + 16 : nullptr;
+    split = split && c.k > (uint32_t)kSplitJ;
     const size_t bin_lds = probe_bin_lds_bytes(tc.T, c.k, STAGE);
-    if (bin_lds > kMaxBlockLds) return fail(NB_ERR_UNSUPPORTED, "tiled probe: LDS of the shape");
+    const size_t lds1 = probe_bin_lds_bytes(tc.T, probe_keff(c.k, 0, kSplitJ, kSplitKPT), STAGE);
+    const size_t lds2 = probe_bin_lds_bytes(tc.T, probe_keff(c.k, kSplitJ, 0, 1), STAGE);
+    if (bin_lds > kMaxBlockLds || (split && lds1 > kMaxBlockLds))
+        return fail(NB_ERR_UNSUPPORTED, "tiled probe: LDS of the shape");
     const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
     auto bin = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR>;
-    auto bin1 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, kSplitJ, false, 1>;
-    auto bin2 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, kSplitJ, 0, true, 2>;
+    auto bin1 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, kSplitJ, false, kSplitKPT>;
+    auto bin2 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, kSplitJ, 0, true, 1, !STAGE>;
     auto tile = probe_tile_kernel<kTileThreads>;
-    split = split && c.k > (uint32_t)kSplitJ;
-    if (split && (size_t)chunk * 16 > ws->probe_state_bytes) {
-        NB_HIP(hipStreamSynchronize(st));  // (the old buffer may be in use on the stream)
-        if ((rc = grow(*ws, &ws->probe_state, &ws->probe_state_bytes, (size_t)chunk * 16))) return rc;
-    }
-    if ((rc = allow_lds(bin, bin_lds)) || (rc = allow_lds(bin1, bin_lds)) || (rc = allow_lds(bin2, bin_lds)) ||
-        (rc = allow_lds(tile, tile_lds)))
+    if ((rc = allow_lds(bin, bin_lds)) || (split && (rc = allow_lds(bin1, lds1))) ||
+        (split && (rc = allow_lds(bin2, lds2))) || (rc = allow_lds(tile, tile_lds)) ||
+        (split && compact && (rc = allow_lds(probe_compact_kernel, kCompactLds))))
         return rc;
     const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
     uint64_t *bk = reinterpret_cast<uint64_t *>(ws->buckets);
@@ -2507,9 +2571,18 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
         const uint64_t *co = offsets ? offsets + done : nullptr;
         for (int round = 0; round < (split ? 2 : 1); ++round) {
             auto b = !split ? bin : round == 0 ? bin1 : bin2;
-            hipLaunchKernelGGL(b, dim3((uint32_t)((cn + NT - 1) / NT)), dim3(NT), bin_lds, st, ck, co,
-                               key_len, cn, c, tc, sc, bk, words, out + done, gate,
-                               split ? reinterpret_cast<uint4 *>(ws->probe_state) : nullptr);
+            const uint64_t kpb = split && round == 0 ? (uint64_t)NT * kSplitKPT : NT;
+            if (round == 1 && compact) {  // the survivors of round one
+                NB_HIP(hipMemsetAsync(nlive, 0, 4, st));
+                const uint64_t per = (uint64_t)kCompactThreads * kCompactPer;
+                hipLaunchKernelGGL(probe_compact_kernel, dim3((uint32_t)((cn + per - 1) / per)),
+                                   dim3(kCompactThreads), kCompactLds, st, out + done, (uint32_t)cn, ids, nlive,
+                                   gate);
+                NB_HIP(hipGetLastError());
+            }
+            hipLaunchKernelGGL(b, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT),
+                               !split ? bin_lds : round == 0 ? lds1 : lds2, st, ck, co,
+                               key_len, cn, c, tc, sc, bk, words, out + done, gate, ids, nlive);
             NB_HIP(hipGetLastError());
             hipLaunchKernelGGL(tile, dim3(tc.T), dim3(kTileThreads), tile_lds, st, tc, sc,
                                (const uint64_t *)bk, words, nwords, out + done, gate);
@@ -2533,11 +2606,12 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     const bool tiled_ok = kTiledLayout && c.k <= kmax && pT <= kMaxTiles &&
                           probe_bin_lds_bytes(pT, c.k, !vec_layout(LAYOUT)) <= kMaxBlockLds;
     const ProbeGate none{nullptr, nullptr, 0, 0, 0};
-    const uint32_t pct = (uint32_t)std::min<uint64_t>(knob(nb::kKnobProbeTiledPct), 101);
-    // the split path takes part in auto's choice for the k <= 8 tiled kernels (C3 / C4's
-    // filters: k = 7); on C5's shape (32-byte keys, k = 10) it lost at every mix
-    const uint32_t split_pct = c.k <= 8 && c.k > (uint32_t)kSplitJ
-                                   ? (uint32_t)std::min<uint64_t>(knob(nb::kKnobProbeSplitPct), 101) : 101u;
+    uint32_t pct = (uint32_t)std::min<uint64_t>(knob(nb::kKnobProbeTiledPct), 101);
+    // the split path takes part in auto's choice wherever the tiled path does (k > 2)
+    const uint64_t spk = knob(nb::kKnobProbeSplitPct);
+    const uint32_t split_pct = c.k <= (uint32_t)kSplitJ ? 101u
+                               : spk ? (uint32_t)std::min<uint64_t>(spk, 101) : split_pct_policy(c.k);
+    if (split_pct <= 100) pct = split_tiled_pct(c.k);
     if (path == 1 || !tiled_ok || (path == 0 && n < kProbeTiledMin))
         return launch_probe_lane<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, out, st, none);
     auto tiled = [&](const uint8_t *k_, const uint64_t *o_, uint64_t n_, uint8_t *out_,
@@ -2767,7 +2841,6 @@ int nb_shutdown(void) {
                 if (e) (void)hipEventDestroy(e);
             if (w->zeroed_alt) (void)hipFree(w->zeroed_alt);
             if (w->buckets_alt) (void)hipFree(w->buckets_alt);
-            if (w->probe_state) (void)hipFree(w->probe_state);
             if (w->probe_hits) (void)hipFree(w->probe_hits);
             if (w->probe_hits_host) (void)hipHostFree(w->probe_hits_host);
             if (w->ev_probe) (void)hipEventDestroy(w->ev_probe);

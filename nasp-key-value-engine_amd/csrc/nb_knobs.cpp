@@ -27,7 +27,7 @@ constexpr KnobDef kDefs[nb::kKnobCount] = {
     {"NB_OVERLAP", 6},       {"NB_SUBPASSES", 0},
     {"NB_TILE_COUNT", 0},
     {"NB_PROBE_PATH", 0},    {"NB_PROBE_CHUNK", 0}, {"NB_PROBE_TILED_PCT", 30},
-    {"NB_PROBE_SPLIT_PCT", 13},
+    {"NB_PROBE_SPLIT_PCT", 0},
     {"NB_FAIL_BUILDS", 0},   {"NB_FAIL_MERKLES", 0},
 };
 

@@ -158,7 +158,7 @@ def test_knob_defaults(built):
     (NB_TILE_COUNT 0), the sub-pass policy (NB_SUBPASSES 0: 2 for multi-pass builds, 1
     for a single pass -- 0 is the policy, not one sub-pass), the tiled probe's pass
     policy (NB_PROBE_CHUNK 0), auto's tiled threshold (NB_PROBE_TILED_PCT 30) and its
-    split-path threshold (NB_PROBE_SPLIT_PCT 13) --
+    split-path threshold (NB_PROBE_SPLIT_PCT 0: the policy) --
     unless the environment of this process set them.  The switches of the variants
     round 5 removed (measured slower) are refused as unknown names."""
     import nasp_bloom as nbm
@@ -168,7 +168,7 @@ def test_knob_defaults(built):
     if "NB_PROBE_TILED_PCT" not in os.environ:
         assert nbm.get_knob("NB_PROBE_TILED_PCT") == 30
     if "NB_PROBE_SPLIT_PCT" not in os.environ:
-        assert nbm.get_knob("NB_PROBE_SPLIT_PCT") == 13
+        assert nbm.get_knob("NB_PROBE_SPLIT_PCT") == 0
     with nbm.knobs(NB_TILE_COUNT=768):
         assert nbm.get_knob("NB_TILE_COUNT") == 768
     for gone in ("NB_BIN_PIPE", "NB_BIN_MIX", "NB_BUCKET_GMAJOR", "NB_FINE_BITS"):

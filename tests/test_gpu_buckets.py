@@ -89,10 +89,12 @@ def test_buckets_spill(dev, oracle, knobs, m, k, kl, extra):
     np.testing.assert_array_equal(got, oracle.build(0, buf, None, kl, n, m, k, SEED))
 
 
+@pytest.mark.parametrize("path", ["tiled", "split"])
 @pytest.mark.parametrize("chunk", ["0", "1000000"])
-def test_buckets_tiled_probe(dev, oracle, knobs, chunk):
+def test_buckets_tiled_probe(dev, oracle, knobs, chunk, path):
     """The tiled probe in key-range passes: a filter of 60 % of 4.5M keys probed
-    over all of them, bit-exact."""
+    over all of them, bit-exact; the split path's second round runs each pass over
+    that pass's compacted survivors (ids relative to the pass)."""
     import torch
     import nasp_bloom as nbm
     n, m, k, kl = 4_500_000, 958_505_838, 7, 16
@@ -103,7 +105,7 @@ def test_buckets_tiled_probe(dev, oracle, knobs, chunk):
     nbm.build_device(t_u8(buf, dev), None, kl, npres, m, k, SEED, 0, wt)
     torch.cuda.synchronize()
     words = wt.cpu().numpy().view(np.uint64)
-    knobs(NB_PROBE_PATH="tiled", NB_PROBE_CHUNK=chunk)
+    knobs(NB_PROBE_PATH=path, NB_PROBE_CHUNK=chunk)
     got = dev_probe(dev, buf, None, kl, n, m, k, SEED, words, 0)
     np.testing.assert_array_equal(got, oracle.probe(0, buf, None, kl, n, m, k, SEED, words))
     assert got[:npres].all()

@@ -145,15 +145,16 @@ def test_probe_32byte_keys_large_k_full_filter(dev, oracle, knobs, path, k):
     assert got[:npres].all()
 
 
-@pytest.mark.parametrize("split_pct", ["13", "101"])
+@pytest.mark.parametrize("shape", ["c4_fixed16", "c5_fixed32_k10"])
+@pytest.mark.parametrize("split_pct", ["0", "101"])
 @pytest.mark.parametrize("pc", [5, 30, 70])
-def test_auto_mixed_batches(dev, oracle, knobs, probe_shapes, pc, split_pct):
+def test_auto_mixed_batches(dev, oracle, knobs, probe_shapes, pc, split_pct, shape):
     """Auto on batches whose sample sees pc % present keys (every key i with
-    i % 20 < pc / 5 present): lane, split (NB_PROBE_SPLIT_PCT 13: 13-50 %) or tiled,
-    bit-exact against the oracle whichever it picks; NB_PROBE_SPLIT_PCT=101 leaves
-    the two-way choice."""
+    i % 20 < pc / 5 present): lane, split (NB_PROBE_SPLIT_PCT 0, the policy: from 7 %
+    at k <= 8, 18 % above, to 65 % / 55 %) or tiled, bit-exact against the oracle whichever it
+    picks; NB_PROBE_SPLIT_PCT=101 leaves the two-way choice."""
     from nasp_bloom import synth
-    buf, offs, kl, n, m, k, fl = probe_shapes["c4_fixed16"]
+    buf, offs, kl, n, m, k, fl = probe_shapes[shape]
     knobs(NB_PROBE_PATH="auto", NB_PROBE_SPLIT_PCT=split_pct)
     npres = n // 2
     words = device_words(dev, buf, None, kl, npres, m, k, fl)
