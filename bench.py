@@ -222,9 +222,10 @@ def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=
     a_o = torch.from_numpy(a_offs.view(np.int64)).to(dev) if a_offs is not None else None
     out_t = torch.empty(wl.n, dtype=torch.uint8, device=dev)
     batches = [("present", keys, offs), ("absent", absent, a_o)]
-    if offs is None and a_o is None and wl.n % 10 == 0 and keys.numel() == wl.n * key_len:
-        mixed = absent.clone()
-        mv, kv = mixed.view(wl.n // 10, 10, key_len), keys.view(wl.n // 10, 10, key_len)
+    nb = wl.n * key_len
+    if offs is None and a_o is None and wl.n % 10 == 0 and min(keys.numel(), absent.numel()) >= nb:
+        mixed = absent.clone()  # (the key buffers carry a few bytes of tail padding)
+        mv, kv = mixed[:nb].view(wl.n // 10, 10, key_len), keys[:nb].view(wl.n // 10, 10, key_len)
         mv[:, :3] = kv[:, :3]
         batches.append(("p30", mixed, None))
     res = {}
