@@ -2607,9 +2607,12 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
                           probe_bin_lds_bytes(pT, c.k, !vec_layout(LAYOUT)) <= kMaxBlockLds;
     const ProbeGate none{nullptr, nullptr, 0, 0, 0};
     uint32_t pct = (uint32_t)std::min<uint64_t>(knob(nb::kKnobProbeTiledPct), 101);
-    // the split path takes part in auto's choice wherever the tiled path does (k > 2)
+    // the split path takes part in auto's choice for register-loaded keys (16 / 32
+    // bytes, k > 2), whose second round runs over the compacted survivors; staged
+    // variable-length keys re-read and gate every key in it, and there it beats both
+    // other paths only between ~25 and ~32 % present (C3, profiles/r05x_bench_c3.json)
     const uint64_t spk = knob(nb::kKnobProbeSplitPct);
-    const uint32_t split_pct = c.k <= (uint32_t)kSplitJ ? 101u
+    const uint32_t split_pct = c.k <= (uint32_t)kSplitJ || !vec_layout(LAYOUT) ? 101u
                                : spk ? (uint32_t)std::min<uint64_t>(spk, 101) : split_pct_policy(c.k);
     if (split_pct <= 100) pct = split_tiled_pct(c.k);
     if (path == 1 || !tiled_ok || (path == 0 && n < kProbeTiledMin))

@@ -52,7 +52,7 @@ enum Knob : int {
     kKnobProbeChunk,    // NB_PROBE_CHUNK    0: tiled-probe pass policy, else keys per pass
     kKnobProbeTiledPct, // NB_PROBE_TILED_PCT auto: the tiled path from this % of the sample
                         //                   present (default 30; 50 before round 4's end)
-    kKnobProbeSplitPct, // NB_PROBE_SPLIT_PCT auto, k > 2: the split tiled path from this %
+    kKnobProbeSplitPct, // NB_PROBE_SPLIT_PCT auto, 16/32-byte keys, k > 2: split from this %
                         //                   present up to 65 % (55 % for k > 8), then tiled;
                         //                   0 (default): the policy, 7 % for k <= 8 and
                         //                   18 % above; > 100: never split
