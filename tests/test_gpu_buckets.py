@@ -109,3 +109,32 @@ def test_buckets_tiled_probe(dev, oracle, knobs, chunk, path):
     got = dev_probe(dev, buf, None, kl, n, m, k, SEED, words, 0)
     np.testing.assert_array_equal(got, oracle.probe(0, buf, None, kl, n, m, k, SEED, words))
     assert got[:npres].all()
+
+
+@pytest.mark.parametrize("chunk", ["0", "900001"])
+def test_split_probe_unaligned_answers(dev, oracle, knobs, chunk):
+    """The split probe's survivor compaction reads the answers four bytes at a time
+    only when they are 4-byte aligned: an answer buffer starting one byte into its
+    allocation, an odd key count and key-range passes of an odd size (so every pass
+    after the first starts unaligned too) take the byte-wise path, bit-exact against
+    the oracle (BloomFilter::possiblyContains, BloomFilter.cpp:67-80)."""
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    n, m, k, kl = 4_500_003, 958_505_838, 7, 16
+    buf = synth.fixed_keys(n, kl, seed=34)
+    npres = int(n * 0.3)
+    wt = torch.zeros(nbm.nwords(m), dtype=torch.int64, device=dev)
+    nbm.build_device(t_u8(buf, dev), None, kl, npres, m, k, SEED, 0, wt)
+    torch.cuda.synchronize()
+    words = wt.cpu().numpy().view(np.uint64)
+    knobs(NB_PROBE_PATH="split", NB_PROBE_CHUNK=chunk)
+    backing = torch.full((n + 8,), 7, dtype=torch.uint8, device=dev)
+    out = backing[1:n + 1]
+    nbm.probe_device(t_u8(buf, dev), None, kl, n, m, k, SEED, 0, wt, out)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    np.testing.assert_array_equal(got, oracle.probe(0, buf, None, kl, n, m, k, SEED, words))
+    assert got[:npres].all()
+    b = backing.cpu().numpy()
+    assert b[0] == 7 and (b[n + 1:] == 7).all()  # nothing written outside the answers
