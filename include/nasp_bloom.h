@@ -79,9 +79,10 @@ uint64_t nb_device_merkle_count(void);
  * environment variable of the same name once, on first use; nb_set_knob changes
  * it for the whole process afterwards (thread-safe).  Names: NB_BUILD_PATH
  * (0 auto, 1 atomic, 2 tiled), NB_PROBE_PATH (0 auto, 1 one lane per key, 2 tiled,
- * 3 split: the tiled probe in two rounds), NB_PROBE_SPLIT_PCT (auto, 16- or 32-byte
- * keys, k > 2: the split path from this percentage of present keys in its sample up
- * to 65, 55 for k > 8; default 0, the policy: 7 for k <= 8, 18 above; > 100: never),
+ * 3 split: the tiled probe in two rounds), NB_PROBE_SPLIT_PCT (auto, k > 2: the split
+ * path from this percentage of present keys in its sample up to 65 for 16- / 32-byte
+ * keys at k <= 8, 55 above, 40 for variable-length keys; default 0, the policy: 7 for
+ * 16- / 32-byte keys at k <= 8, 18 otherwise; > 100: never),
  * NB_PROBE_CHUNK (keys per tiled-probe pass; 0: the policy), NB_PROBE_TILED_PCT (auto's
  * tiled path from this percentage of present keys in its sample when it never splits,
  * default 30),
@@ -227,11 +228,10 @@ int nb_build_device_ex(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_
  * rate for present keys, ~half of it for absent ones) or, for k > 2, the split tiled
  * path (two rounds: every key's first two indices, then the rest for the keys still
  * possibly present); NB_PROBE_PATH=0 (auto) probes the first 4 096 keys one lane per
- * key and picks from the share of them present: for 16- and 32-byte keys the lane path
- * below NB_PROBE_SPLIT_PCT
- * (the policy: 7 % for k <= 8, 18 % above), the split path up to 65 % (55 % for
- * k > 8), the tiled path from there (variable-length keys, or NB_PROBE_SPLIT_PCT >
- * 100: the tiled path from NB_PROBE_TILED_PCT, 30 %).  Auto waits once for that sample (its 16 counts land in
+ * key and picks from the share of them present: the lane path below NB_PROBE_SPLIT_PCT
+ * (the policy: 7 % for 16- / 32-byte keys at k <= 8, 18 % otherwise), the split path
+ * up to 65 % (55 % for k > 8, 40 % for variable-length keys), the tiled path from
+ * there (NB_PROBE_SPLIT_PCT > 100: the tiled path from NB_PROBE_TILED_PCT, 30 %).  Auto waits once for that sample (its 16 counts land in
  * host-mapped memory) -- except while the stream is being captured into a graph, where
  * every path is launched and gated on the sample on the device.  Same answers on every
  * path. */

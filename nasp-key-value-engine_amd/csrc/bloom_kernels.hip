@@ -260,12 +260,14 @@ struct ProbeGate {
                                // to pct, where the tiled path takes over
 };
 // Auto's thresholds with the split path, per shape (the crossings of
-// profiles/r05_probe_split_final_{c4,c5shape}.txt): lane -> split at ~6 % present on
-// C4's filter (16-byte keys, k = 7) and ~18 % on C5's shape (32-byte keys, k = 10: the
-// lane kernel's absent keys are cheap there) -- NB_PROBE_SPLIT_PCT 0, the policy --
-// and split -> tiled at ~67 % / ~55 %.
-constexpr uint32_t split_pct_policy(uint32_t k) { return k <= 8 ? 7u : 18u; }
-constexpr uint32_t split_tiled_pct(uint32_t k) { return k <= 8 ? 65u : 55u; }
+// profiles/r05_probe_split_final_{c4,c5shape}.txt and r05_probe_split_c3.txt): lane ->
+// split at ~6 % present on C4's filter (16-byte keys, k = 7), ~18 % on C5's shape
+// (32-byte keys, k = 10: the lane kernel's absent keys are cheap there) and on C3's
+// variable-length keys -- NB_PROBE_SPLIT_PCT 0, the policy -- and split -> tiled at
+// ~67 % / ~55 % / ~40 % (the second round hashes a listed variable-length key straight
+// from HBM, without the stage).
+constexpr uint32_t split_pct_policy(uint32_t k, bool vec) { return vec && k <= 8 ? 7u : 18u; }
+constexpr uint32_t split_tiled_pct(uint32_t k, bool vec) { return !vec ? 40u : k <= 8 ? 65u : 55u; }
 // Auto's choice from the sample's hit count h of s keys: 1 lane, 2 tiled, 3 split.
 // Without the split path: tiled when at least pct % were present (a present key costs
 // the lane kernel ~k gathers, an absent one ~2, and the tiled path a fixed pass plus
@@ -850,9 +852,10 @@ __device__ __forceinline__ void bin_tail_two_tiles(uint32_t *lds, uint32_t sort_
 // The split tiled probe (round 5) counts a range of each key's indices: J0 is the
 // first one counted (the earlier ones only advance the generator; KX, when set, is
 // the end), and with GATE a key is counted only while gate[kid] != 0 (its answer
-// after the first round); live[p] says whether slot p was counted.  With IDS
-// (register-loaded keys only) the launch's keys are ids[0, n): the second round over
-// the compacted list of the keys the first left at 1 (probe_compact_kernel).
+// after the first round); live[p] says whether slot p was counted.  With IDS the
+// launch's keys are ids[0, n): the second round over the compacted list of the keys
+// the first left at 1 (probe_compact_kernel); keys of a staged layout are then hashed
+// straight from HBM (a block's listed keys are not one contiguous byte range).
 template <int FLAVOR, int LAYOUT, int KPT, int NT, bool STAGE, int KR, int KX = 0, int J0 = 0,
           bool GATE = false, bool IDS = false>
 struct BinPhase1 {
@@ -860,7 +863,6 @@ struct BinPhase1 {
     static_assert(KR == 0 || (uint64_t)KPT * NT * (KX ? KX - J0 : KR) < (1u << (kHandleShift - 2)),
                   "a block's ranks must fit the placement handle's low bits");
     static_assert(J0 == 0 || KR > 0, "an index range needs the rank registers");
-    static_assert(!IDS || !STAGE, "a key list needs register-loaded keys");
     IndexGen gen[KPT];
     uint32_t ridx[KPT][kR], rank[KPT][kR];
     uint32_t kid[KPT];  // (mod 2^32: the probe launches chunks of < 2^32 keys)
@@ -927,14 +929,18 @@ struct BinPhase1 {
                 }
             }
         };
-        if (!STAGE) {
+        if (!STAGE || IDS) {
             // every key of the lane hashed before any count atomic is issued: the
             // compiler otherwise drains key p's LDS atomics (s_waitcnt lgkmcnt(0) at the
             // join of the i < n branch) before it hashes key p + 1
             uint64_t h1[KPT], h2[KPT];
 #pragma unroll
-            for (int p = 0; p < KPT; ++p)  // (a lane past n hashes its stale registers)
-                kb.hash(c, keys, key_len, base + (uint64_t)p * NT + tid, p, &h1[p], &h2[p]);
+            for (int p = 0; p < KPT; ++p) {  // (a lane past n hashes its stale registers --
+                // key words in registers only; a pointer layout's dead lane reads nothing)
+                if (vec_layout(LAYOUT) || live[p])
+                    kb.hash(c, keys, key_len, IDS ? (uint64_t)kid[p] : base + (uint64_t)p * NT + tid, p,
+                            &h1[p], &h2[p]);
+            }
 #pragma unroll
             for (int p = 0; p < KPT; ++p)
                 if (live[p]) count_key(p, h1[p], h2[p]);
@@ -2538,12 +2544,12 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
     const uint64_t passes = (n + budget - 1) / budget;
     const uint64_t chunk = std::max<uint64_t>(1, (n + passes - 1) / passes);
     const TileCfg tc = probe_tiles(c.fm.m, chunk, c.k);
-    // register-loaded keys: the split path's second round runs over the compacted list
-    // of the first round's survivors -- a count word, then the ids -- kept in the
-    // workspace's second bucket array (the two-level build's; unused by the probe) and
-    // reserved on every tiled probe of such a shape, so that a warm-up on the one-round
-    // path sizes it for a later capture of auto's gated paths
-    const bool compact = !STAGE && c.k > (uint32_t)kSplitJ;
+    // the split path's second round runs over the compacted list of the first round's
+    // survivors -- a count word, then the ids -- kept in the workspace's second bucket
+    // array (the two-level build's; unused by the probe) and reserved on every tiled
+    // probe with k > 2, so that a warm-up on the one-round path sizes it for a later
+    // capture of auto's gated paths
+    const bool compact = c.k > (uint32_t)kSplitJ;
     const size_t ids_bytes = compact ? (chunk + 16) * 4 : 0;
     if ((rc = ws_reserve(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * 8, &sc, ids_bytes))) return rc;
     uint32_t *nlive = compact ? reinterpret_cast<uint32_t *>(ws->buckets2) : nullptr;
@@ -2557,7 +2563,7 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
     const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
     auto bin = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR>;
     auto bin1 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, kSplitJ, false, kSplitKPT>;
-    auto bin2 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, kSplitJ, 0, true, 1, !STAGE>;
+    auto bin2 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, kSplitJ, 0, true, 1, true>;
     auto tile = probe_tile_kernel<kTileThreads>;
     if ((rc = allow_lds(bin, bin_lds)) || (split && (rc = allow_lds(bin1, lds1))) ||
         (split && (rc = allow_lds(bin2, lds2))) || (rc = allow_lds(tile, tile_lds)) ||
@@ -2607,14 +2613,12 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
                           probe_bin_lds_bytes(pT, c.k, !vec_layout(LAYOUT)) <= kMaxBlockLds;
     const ProbeGate none{nullptr, nullptr, 0, 0, 0};
     uint32_t pct = (uint32_t)std::min<uint64_t>(knob(nb::kKnobProbeTiledPct), 101);
-    // the split path takes part in auto's choice for register-loaded keys (16 / 32
-    // bytes, k > 2), whose second round runs over the compacted survivors; staged
-    // variable-length keys re-read and gate every key in it, and there it beats both
-    // other paths only between ~25 and ~32 % present (C3, profiles/r05x_bench_c3.json)
+    // the split path takes part in auto's choice wherever the tiled path does (k > 2)
+    constexpr bool kVec = vec_layout(LAYOUT);
     const uint64_t spk = knob(nb::kKnobProbeSplitPct);
-    const uint32_t split_pct = c.k <= (uint32_t)kSplitJ || !vec_layout(LAYOUT) ? 101u
-                               : spk ? (uint32_t)std::min<uint64_t>(spk, 101) : split_pct_policy(c.k);
-    if (split_pct <= 100) pct = split_tiled_pct(c.k);
+    const uint32_t split_pct = c.k <= (uint32_t)kSplitJ ? 101u
+                               : spk ? (uint32_t)std::min<uint64_t>(spk, 101) : split_pct_policy(c.k, kVec);
+    if (split_pct <= 100) pct = split_tiled_pct(c.k, kVec);
     if (path == 1 || !tiled_ok || (path == 0 && n < kProbeTiledMin))
         return launch_probe_lane<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, out, st, none);
     auto tiled = [&](const uint8_t *k_, const uint64_t *o_, uint64_t n_, uint8_t *out_,

@@ -52,10 +52,11 @@ enum Knob : int {
     kKnobProbeChunk,    // NB_PROBE_CHUNK    0: tiled-probe pass policy, else keys per pass
     kKnobProbeTiledPct, // NB_PROBE_TILED_PCT auto: the tiled path from this % of the sample
                         //                   present (default 30; 50 before round 4's end)
-    kKnobProbeSplitPct, // NB_PROBE_SPLIT_PCT auto, 16/32-byte keys, k > 2: split from this %
-                        //                   present up to 65 % (55 % for k > 8), then tiled;
-                        //                   0 (default): the policy, 7 % for k <= 8 and
-                        //                   18 % above; > 100: never split
+    kKnobProbeSplitPct, // NB_PROBE_SPLIT_PCT auto, k > 2: the split path from this % present
+                        //                   up to 65 % (55 % for k > 8, 40 % for variable-
+                        //                   length keys), then tiled; 0 (default): the
+                        //                   policy, 7 % for 16-/32-byte keys at k <= 8, 18 %
+                        //                   otherwise; > 100: never split
     kKnobFailBuilds,    // NB_FAIL_BUILDS    fault injection: the next N device builds fail
                         //                   with NB_ERR_HIP before launching anything
     kKnobFailMerkles,   // NB_FAIL_MERKLES   the same for device Merkle trees

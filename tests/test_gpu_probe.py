@@ -167,3 +167,22 @@ def test_auto_mixed_batches(dev, oracle, knobs, probe_shapes, pc, split_pct, sha
     want = oracle.probe(fl, mixed, None, kl, n, m, k, SEED, words)
     np.testing.assert_array_equal(got, want)
     assert got[idx].all()
+
+
+@pytest.mark.parametrize("pc", [5, 30, 70])
+def test_auto_mixed_batches_varlen(dev, oracle, knobs, probe_shapes, pc):
+    """The same for variable-length keys (C3's shape): the filter of all the keys, the
+    batch the same keys with the first byte changed except where i % 20 < pc / 5 --
+    lane, split (18-40 %: its second round hashes the listed keys straight from HBM) or
+    tiled, bit-exact against the oracle."""
+    buf, offs, kl, n, m, k, fl = probe_shapes["c3_varlen"]
+    knobs(NB_PROBE_PATH="auto", NB_PROBE_SPLIT_PCT="0")
+    words = device_words(dev, buf, offs, kl, n, m, k, fl)
+    keep = np.arange(n) % 20 < pc // 5
+    mixed = buf.copy()
+    starts = offs[:-1].astype(np.int64)
+    mixed[starts[~keep]] ^= 0x5A
+    got = dev_probe(dev, mixed, offs, kl, n, m, k, SEED, words, fl)
+    want = oracle.probe(fl, mixed, offs, kl, n, m, k, SEED, words)
+    np.testing.assert_array_equal(got, want)
+    assert got[keep].all()

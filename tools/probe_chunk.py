@@ -33,10 +33,12 @@ def main():
     ap.add_argument("--no-lane", action="store_true")
     ap.add_argument("--split", action="store_true", help="also the split tiled probe (two rounds)")
     ap.add_argument("--auto-pct", default="", help="auto path at these NB_PROBE_TILED_PCT values")
-    ap.add_argument("--workload", default="c4", choices=["c4", "c5"],
+    ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c3"],
                     help="c4: C4's filter from the 100M probed present keys; c5: C5's shape "
                          "(m = 2^32-1, k = 10, 32-byte keys), --n probed keys, the filter built "
-                         "from --fill-keys device-random keys (the present keys among them)")
+                         "from --fill-keys device-random keys (the present keys among them); c3: "
+                         "C3's 100M variable-length keys (8-64 B) and filter, the absent keys "
+                         "the same keys with their first byte changed (same offsets)")
     ap.add_argument("--n", type=int, default=50_000_000)
     ap.add_argument("--fill-keys", type=int, default=400_000_000)
     args = ap.parse_args()
@@ -44,7 +46,22 @@ def main():
     dev = torch.device("cuda", 0)
     st = torch.cuda.Stream(device=dev)
     fill = None
-    if args.workload == "c4":
+    offs = None
+    if args.workload == "c3":
+        wl = synth.C3
+        p_np, o_np, kl = synth.keys_for(wl)
+        present = torch.from_numpy(p_np).to(dev)
+        offs = torch.from_numpy(o_np.view(np.int64)).to(dev)
+        starts = offs[:-1]
+
+        def flipped(mask):  # the keys where mask holds, first byte changed
+            b = present.clone()
+            sel = starts[mask]
+            b[sel] = b[sel] ^ 0x5A
+            return b
+        keyno = torch.arange(wl.n, device=dev)
+        absent = flipped(torch.ones(wl.n, dtype=torch.bool, device=dev))
+    elif args.workload == "c4":
         wl = synth.C4
         p_np, _, kl = synth.keys_for(wl)
         a_np, _, _ = synth.keys_for(wl, seed=synth.SEED + 1000)
@@ -59,13 +76,19 @@ def main():
         fill = torch.randint(0, 256, (args.fill_keys * kl + 64,), dtype=torch.uint8, device=dev, generator=g)
         present = fill[:wl.n * kl + 64].clone()
         absent = torch.randint(0, 256, (wl.n * kl + 64,), dtype=torch.uint8, device=dev, generator=g)
-    mixed = present.clone()
-    mv = mixed[:wl.n * kl].view(wl.n, kl)
-    mv[1::2] = absent[:wl.n * kl].view(wl.n, kl)[1::2]
-    batches = {"present": present, "absent": absent, "mixed": mixed}
     want_b = args.batches.split(",")
+    if offs is not None:
+        batches = {"present": present, "absent": absent, "mixed": flipped(keyno % 2 == 1)}
+        for pc in range(10, 100, 10):
+            if f"p{pc}" in want_b:
+                batches[f"p{pc}"] = flipped(keyno % 10 >= pc // 10)
+    else:
+        mixed = present.clone()
+        mv = mixed[:wl.n * kl].view(wl.n, kl)
+        mv[1::2] = absent[:wl.n * kl].view(wl.n, kl)[1::2]
+        batches = {"present": present, "absent": absent, "mixed": mixed}
     for pc in range(10, 100, 10):  # pc % present: keys i with i % 10 < pc / 10 (the sample sees the same mix)
-        if f"p{pc}" not in want_b:
+        if f"p{pc}" not in want_b or offs is not None:
             continue
         b = absent.clone()
         bv, pv = b[:wl.n * kl].view(wl.n // 10, 10, kl), present[:wl.n * kl].view(wl.n // 10, 10, kl)
@@ -74,7 +97,7 @@ def main():
     batches = {b: batches[b] for b in args.batches.split(",")}
     words = torch.zeros(nbm.nwords(wl.m), dtype=torch.int64, device=dev)
     if fill is None:
-        nbm.build_device(present, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, stream=st,
+        nbm.build_device(present, offs, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, stream=st,
                          overwrite=True)
     else:
         nbm.build_device(fill, None, kl, args.fill_keys, wl.m, wl.k, synth.H2_SEED, 0, words, stream=st,
@@ -88,7 +111,7 @@ def main():
     ref = {}
     with nbm.knobs(NB_PROBE_PATH="lane"):
         for name, b in batches.items():
-            nbm.probe_device(b, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out, stream=st)
+            nbm.probe_device(b, offs, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out, stream=st)
             torch.cuda.synchronize(dev)
             ref[name] = out.clone()
     variants = ([] if args.no_lane else [("lane", "lane", 0, "30", {})]) + [
@@ -101,14 +124,14 @@ def main():
         for label, path, chunk, pct, extra in variants:
             with nbm.knobs(NB_PROBE_PATH=path, NB_PROBE_CHUNK=str(chunk), NB_PROBE_TILED_PCT=pct, **extra):
                 for name, b in batches.items():
-                    nbm.probe_device(b, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out, stream=st)
+                    nbm.probe_device(b, offs, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out, stream=st)
                     torch.cuda.synchronize(dev)
                     if not torch.equal(out, ref[name]):
                         bad += 1
                         print(f"MISMATCH {label} {name}", flush=True)
                     t0 = time.perf_counter()
                     for _ in range(5):
-                        nbm.probe_device(b, None, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out,
+                        nbm.probe_device(b, offs, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out,
                                          stream=st)
                     torch.cuda.synchronize(dev)
                     ms = (time.perf_counter() - t0) * 1e3 / 5
