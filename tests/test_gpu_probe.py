@@ -42,6 +42,7 @@ def shapes():
     return {
         "c4_fixed16": (f16, None, 16, n, 958_505_838, 7, 0),
         "c3_varlen": (var, voffs, 0, n, 958_505_838, 7, 0),
+        "c3_varlen_fnv": (var, voffs, 0, n, 958_505_838, 7, 1),
         "c2_fixed16_fnv": (f16, None, 16, n, 95_850_584, 7, 1),
         "c5_fixed32_k10": (f32, None, 32, n, 2**32 - 1, 10, 0),
     }
@@ -53,7 +54,7 @@ def probe_shapes():
 
 
 @pytest.mark.parametrize("path", ["lane", "tiled", "split", "auto"])
-@pytest.mark.parametrize("shape", ["c4_fixed16", "c3_varlen", "c2_fixed16_fnv", "c5_fixed32_k10"])
+@pytest.mark.parametrize("shape", ["c4_fixed16", "c3_varlen", "c3_varlen_fnv", "c2_fixed16_fnv", "c5_fixed32_k10"])
 @pytest.mark.parametrize("present_first", [True, False])
 def test_probe_paths_match_oracle(dev, oracle, knobs, probe_shapes, path, shape, present_first):
     """A filter of 60 % of the batch's keys, probed over all of them: present keys,
