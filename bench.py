@@ -9,7 +9,9 @@ at N GPUs exactly BASELINE config 4 (one independent SSTable filter per GPU).
 
 One step = one pass of the hot path over one batch: build a fresh filter from
 every key of the batch (hash + index + bit scatter + filter store; the library's
-overwrite mode, so no separate clear pass), keys already resident in HBM.  N > 1 (torchrun, one rank per GPU): every rank builds
+overwrite mode, so no separate clear pass), keys already resident in HBM.  N > 1 (one rank
+per GPU: `--gpus N` starts the N ranks itself as a torch.distributed.run child process
+when no launcher is around it, and refuses a launcher's WORLD_SIZE != N): every rank builds
 its own independent filter over its own keys (the compaction fan-out, C4) --
 weak scaling, no data-path collective.  `value` = all keys of all ranks / the
 max-over-ranks time of the K timed steps.
@@ -351,6 +353,59 @@ def emit(obj):
     out.flush()
 
 
+def launch_plan(gpus, argv, env):
+    """What `bench.py --gpus N` does before anything touches torch or the GPU:
+      ("run", None)       -- this process is the (only) rank: N = 1 without a launcher,
+                             or one rank of an external torch.distributed.run whose
+                             WORLD_SIZE equals N;
+      ("launch", cmd)     -- N > 1 and no launcher around us: start N ranks through
+                             torch.distributed.run as a CHILD process (never an exec)
+                             with the same arguments; the parent relays the rank-0 JSON
+                             line and exits with the child's code;
+      ("error", message)  -- WORLD_SIZE is set and differs from N, or N < 1."""
+    if gpus < 1:
+        return "error", f"--gpus must be >= 1 (got {gpus})"
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            return "error", (f"WORLD_SIZE={ws} from the launcher but --gpus {gpus}: "
+                             "refusing to report a line for the wrong GPU count")
+        return "run", None
+    if gpus == 1:
+        return "run", None
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:  # a free rendezvous port
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + list(argv)
+    return "launch", cmd
+
+
+def run_launcher(cmd, json_out):
+    """Runs the N-rank child and relays its output: the rank-0 JSON line (the only
+    stdout line that parses as a JSON object) to our stdout, everything else to stderr,
+    line by line as it arrives.  Returns the child's exit code."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=None, env=env, text=True, bufsize=1)
+    for line in p.stdout:
+        s = line.strip()
+        if s.startswith("{"):
+            try:
+                json.loads(s)
+                json_out.write(s + "\n")
+                json_out.flush()
+                continue
+            except ValueError:
+                pass
+        sys.stderr.write(line)
+        sys.stderr.flush()
+    return p.wait()
+
+
 def main():
     global _JSON_OUT
     sys.stdout.flush()
@@ -375,7 +430,22 @@ def main():
     ap.add_argument("--no-rank-share", action="store_true",
                     help="c5 at N=1: skip the per-rank (1B/8 keys) partial-build line")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="print the launch decision for --gpus as JSON and exit (no GPU use)")
     args = ap.parse_args()
+
+    # --gpus N: N ranks, one per GPU.  Decided before torch is imported: with no
+    # launcher around us the ranks are a torch.distributed.run child process
+    argv = [a for a in sys.argv[1:] if a != "--launch-dry-run"]
+    action, what = launch_plan(args.gpus, argv, os.environ)
+    if args.launch_dry_run:
+        emit({"action": action, "detail": what, "gpus": args.gpus})
+        return 0
+    if action == "error":
+        sys.stderr.write(f"bench.py: {what}\n")
+        return 2
+    if action == "launch":
+        return run_launcher(what, _JSON_OUT)
 
     import torch
     import torch.distributed as dist
@@ -391,6 +461,10 @@ def main():
     backend = os.environ.get("NB_BENCH_BACKEND", "nccl")
     if backend != "nccl":
         local %= max(1, torch.cuda.device_count())
+    elif world > torch.cuda.device_count():  # (counting devices does not initialise HIP)
+        raise SystemExit(f"bench.py: {world} ranks over RCCL need {world} GPUs, "
+                         f"{torch.cuda.device_count()} visible (NB_BENCH_BACKEND=gloo rehearses "
+                         "more ranks than GPUs)")
     if world > 1:
         torch.cuda.set_device(local)
         if backend == "nccl":
@@ -725,4 +799,4 @@ def rank_share_rate(nbm, wl, keys, seed, flavor, dev, stream, world=8, steps=3):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -139,6 +139,12 @@ def build_cooperative(keys: torch.Tensor, offsets: torch.Tensor | None, key_len:
     # kernel on the current stream, which waits for the build first (a caller's
     # non-current build stream is joined, not raced)
     side = stream is not None and keys.is_cuda and stream != torch.cuda.current_stream(keys.device)
+    if side:
+        # the other direction too: the side stream waits for the current
+        # stream's work -- the keys' producer and the padding memset above -- and the
+        # caching allocator learns that `partial` is in use on it
+        stream.wait_stream(torch.cuda.current_stream(keys.device))
+        partial.record_stream(stream)
     _mark(marks, "start", keys.device, stream if side else None)
     if build_fn is None:
         build_device(keys, offsets, key_len, n, m, k, seed, flavor, partial, stream=stream,

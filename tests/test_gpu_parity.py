@@ -783,11 +783,18 @@ def test_cooperative_build_single_rank(dev, oracle):
         torch.cuda.synchronize()
         got = full.cpu().numpy().view(np.uint64)
         np.testing.assert_array_equal(got[: want.size], want)
-    # the build on a caller's non-current stream: the merge (on the current stream)
-    # joins it before the exchange; the phase marks bracket the build on that stream
+    # the build on a caller's non-current stream: it waits for the keys' producer on the
+    # current stream (here a copy queued behind ~10 ms of matmuls, no host
+    # synchronisation: ADVICE r05), and the merge (on the current stream) joins it
+    # before the exchange; the phase marks bracket the build on that stream
     side = torch.cuda.Stream(device=dev)
-    keys = t_u8(buf, dev)
+    src = t_u8(buf, dev)
     torch.cuda.synchronize()
+    keys = torch.zeros_like(src)
+    busy = torch.rand(4096, 4096, device=dev)
+    for _ in range(12):
+        busy = busy @ busy * 1e-3
+    keys.copy_(src)
     marks = []
     full = D.build_cooperative(keys, None, 32, n, synth.C5.m, synth.C5.k, SEED, 0, exchange_single=True,
                                stream=side, marks=marks)
