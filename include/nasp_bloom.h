@@ -84,8 +84,12 @@ uint64_t nb_device_merkle_count(void);
  * keys at k <= 8, 55 above, 40 for variable-length keys; default 0, the policy: 7 for
  * 16- / 32-byte keys at k <= 8, 18 otherwise; > 100: never),
  * NB_PROBE_CHUNK (keys per tiled-probe pass; 0: the policy), NB_PROBE_TILED_PCT (auto's
- * tiled path from this percentage of present keys in its sample when it never splits,
- * default 30),
+ * tiled path from this percentage of present keys in its sample; default 0, the policy:
+ * the split policy's upper bound above, 30 when auto never splits; a split threshold at
+ * or above it leaves the two-way choice), NB_PROBE_ENTRY (tiled-probe bucket entries:
+ * 32, default, or 64 bits), NB_PROBE_BIN_GRID (blocks per CU of the tiled-probe bin
+ * kernels' grid-stride grid; 0: 8), NB_PROBE_HOST_PICK (1: auto reads its sample back
+ * on the host outside graph capture; 0, default: gated on the device),
  * NB_PACK, NB_TILE_BITS, NB_SHARDS, NB_CHUNK_KEYS, NB_TWO_LEVEL, NB_PACK5,
  * NB_ENTRY32, NB_RANK, NB_FIXED32, NB_FPMOD, NB_KEXACT, NB_BIN_WIDE, NB_OVERLAP (two-level
  * sub-passes pipelined over a second stream of the workspace: 0 off, 1/2 normal/high
@@ -231,10 +235,12 @@ int nb_build_device_ex(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_
  * key and picks from the share of them present: the lane path below NB_PROBE_SPLIT_PCT
  * (the policy: 7 % for 16- / 32-byte keys at k <= 8, 18 % otherwise), the split path
  * up to 65 % (55 % for k > 8, 40 % for variable-length keys), the tiled path from
- * there (NB_PROBE_SPLIT_PCT > 100: the tiled path from NB_PROBE_TILED_PCT, 30 %).  Auto waits once for that sample (its 16 counts land in
- * host-mapped memory) -- except while the stream is being captured into a graph, where
- * every path is launched and gated on the sample on the device.  Same answers on every
- * path. */
+ * there (NB_PROBE_SPLIT_PCT > 100: the tiled path from 30 %).  The choice is made on
+ * the device: every path is launched behind the sample and gated on its count, so
+ * auto never waits on the host (NB_PROBE_HOST_PICK=1 restores rounds 3-5's host
+ * read-back outside graph capture).  The tiled paths' bucket entries are 32-bit words
+ * behind one header word per run (NB_PROBE_ENTRY=64: key << 32 | offset).  Same
+ * answers on every path. */
 int nb_probe_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
                     uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
                     const uint64_t *d_words, uint8_t *d_out, void *stream);

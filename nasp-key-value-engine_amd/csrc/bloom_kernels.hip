@@ -548,6 +548,9 @@ struct TileScratch {
     uint32_t *spill32;    // [2*ceil(m/64)] spill bitmap (zero between builds)
     uint64_t *zero_words = nullptr;  // counted tiles, overwrite: the filter, whose words
                                      // holding a tile boundary the bin kernel zeroes
+    uint32_t *vbctr = nullptr;  // tiled probe: [G] bin-block counters of the grid-stride
+                                // bin kernels (zero between launches: the tile kernel
+                                // after each bin kernel resets them)
 };
 
 // Phases 2-4 of the bin kernel in rank mode when T <= 2 NT: thread tid owns the
@@ -1567,6 +1570,100 @@ __host__ __device__ constexpr uint32_t probe_sort_offset_words(uint32_t T) {
     return (4 * T + 32 + 3) & ~3u;  // cnt | S | GX | L | wave_sums, 16-byte aligned
 }
 
+// The E32 probe bin kernel's phases 2-4 (see probe_bin_kernel): cnt[t] already holds
+// each touched tile's run length including its header slot.  Scan, one reservation
+// per run, the run's header slot (by the thread reserving it) and every index placed
+// behind it as its 32-bit entry.  In LDS a header slot holds 0x80000000 | t: the
+// write-out (each wave one contiguous range of slots, 64 at a time) finds a slot's
+// tile with the same "last header" wave scan the tile kernel uses, so the sort area
+// is 4 B per slot -- two blocks of 2 048 keys fit a CU -- and stores the bin block's
+// header word 0x80000000 | vb in its place.  An entry past its bucket's capacity
+// (duplicated keys only) is tested right here.
+__device__ __forceinline__ uint32_t wave_last_nonzero(uint32_t v);
+template <int NT, int PKPT, int KR, int J0, int J1, bool IDS, class PH>
+__device__ __forceinline__ void probe_bin_tail_e32(uint32_t vb, const PH &ph, const TileCfg &tc, const TileScratch &sc,
+                                                   uint32_t *cnt, uint32_t *S, uint32_t *GX, uint32_t *L,
+                                                   uint32_t *wave_sums, uint32_t *sword,
+                                                   uint32_t *__restrict__ buckets,
+                                                   const uint64_t *__restrict__ words,
+                                                   uint8_t *__restrict__ out,
+                                                   const uint32_t *__restrict__ ids, uint64_t base,
+                                                   uint32_t k) {
+    const uint32_t T = tc.T, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
+    const uint32_t shard = vb & (tc.G - 1);
+    uint32_t *cur = sc.gcur + (size_t)shard * T;
+    for (uint32_t t = tid; t < T; t += NT) {
+        const uint32_t h = cnt[t], g = h ? atomicAdd(&cur[t], h) : 0u;
+        GX[t] = bucket_region(tc, t, shard) * tc.cap + g - S[t];
+        L[t] = S[t] + (g < tc.cap ? tc.cap - g : 0u);
+        if (h) sword[S[t]] = 0x80000000u | t;
+    }
+    // placement behind the header slot (the reservations' round trips overlap it)
+    const uint32_t msk = (1u << tc.ts) - 1, b32 = (uint32_t)base;
+#pragma unroll
+    for (int p = 0; p < PKPT; ++p) {
+        if (ph.live[p]) {
+            // the key's position in the block (staged keys: kid is base + its slot)
+            const uint32_t kib = IDS ? (uint32_t)(p * NT) + tid : ph.kid[p] - b32;
+#pragma unroll
+            for (int j = J0; j < KR; ++j)
+                if (J1 ? j < J1 : j < (int)k) {
+                    const uint32_t r = ph.ridx[p][j], t = r >> tc.ts;
+                    sword[S[t] + 1 + ((ph.rank[p][j] & kHandleMask) >> 2)] = (kib << tc.ts) | (r & msk);
+                }
+        }
+    }
+    __syncthreads();
+    constexpr uint32_t kW = NT / 64;
+    const uint32_t per = (total + kW - 1) / kW;
+    const uint32_t s0 = min(wid * per, total), s1 = min(s0 + per, total);
+    if (s0 >= s1) return;  // wave-uniform; no barrier follows
+    // the tile in force at s0 (+1; slot 0 is a header)
+    uint32_t carry = 0;
+    for (uint32_t b = s0; b > 0 && carry == 0; b = b > 64 ? b - 64 : 0) {
+        const bool in = lane < b;
+        const uint32_t w = in ? sword[b - 1 - lane] : 0u;
+        const uint64_t hm = __ballot(in && (w >> 31));
+        if (hm) carry = (__shfl(w, (int)__builtin_ctzll(hm)) & 0x7fffffffu) + 1;
+    }
+    const uint32_t hdr = 0x80000000u | vb;
+    for (uint32_t q0 = s0; q0 < s1; q0 += 64) {
+        const uint32_t q = q0 + lane;
+        const bool valid = q < s1;
+        const uint32_t w = valid ? sword[q] : 0u;
+        const bool is_hdr = valid && (w >> 31);
+        const uint32_t X = wave_last_nonzero(is_hdr ? (w & 0x7fffffffu) + 1 : 0u);
+        const uint32_t t = (X ? X : carry) - 1;
+        const uint32_t tail = __builtin_amdgcn_readlane(X, 63);
+        if (tail) carry = tail;
+        if (!valid) continue;
+        if (q < L[t]) {
+            buckets[(uint32_t)(GX[t] + q)] = is_hdr ? hdr : w;
+        } else if (!is_hdr) {
+            const uint32_t v = (t << tc.ts) | (w & msk);
+            if (!((words[v >> 6] >> (v & 63)) & 1u)) {
+                const uint32_t j = b32 + (w >> tc.ts);
+                out[IDS ? ids[j] : j] = 0;
+            }
+        }
+    }
+}
+
+// Inclusive "last nonzero" scan across a wave64 (the wave_inclusive_scan pattern with
+// a select for the add): lane i gets the value of the highest lane <= i whose input
+// is nonzero, or 0.
+__device__ __forceinline__ uint32_t wave_last_nonzero(uint32_t v) {
+    uint32_t s;
+    s = __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false); v = v ? v : s;  // row_shr:1
+    s = __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false); v = v ? v : s;  // row_shr:2
+    s = __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false); v = v ? v : s;  // row_shr:4
+    s = __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false); v = v ? v : s;  // row_shr:8
+    s = __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false); v = v ? v : s;  // row_bcast:15
+    s = __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false); v = v ? v : s;  // row_bcast:31
+    return v;
+}
+
 // Split probe (round 5): J0..J1 (J1 = 0: k) is the range of each key's indices this
 // launch bins; R2 marks the second round, which bins only the keys whose answer the
 // first round left at 1 and leaves the answers' initialisation to the first.  PKPT
@@ -1576,19 +1673,22 @@ __host__ __device__ constexpr uint32_t probe_sort_offset_words(uint32_t T) {
 // keys): the keys are the compacted list ids[0, *nlive) of the first round's survivors
 // (probe_compact_kernel), so the hash and the runs go to live keys only; the grid is
 // sized for every key of the pass and the blocks past the list return at once.
-template <int FLAVOR, int LAYOUT, bool STAGE, int KR, int J0 = 0, int J1 = 0, bool R2 = false, int PKPT = 1,
-          bool IDS = false>
-__global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) void probe_bin_kernel(
-    const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
-    uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc, uint64_t *__restrict__ buckets,
-    const uint64_t *__restrict__ words, uint8_t *__restrict__ out, ProbeGate gate,
-    const uint32_t *__restrict__ ids, const uint32_t *__restrict__ nlive) {
+// E32 (round 6, NB_PROBE_ENTRY=32): 32-bit bucket entries.  Every run a block writes
+// into a (tile, shard) bucket starts with a header word, bit 31 set, holding the
+// block's index in the launch; the run's entries are kib << ts | in-tile offset, kib
+// the key's position in the block (< NT * PKPT <= 2^(31 - ts)), so the tile kernel
+// (probe_tile32_kernel) recovers the key as header * NT * PKPT + kib (IDS: the
+// list entry ids[header * NT + kib]).  4 B per lookup plus a header per run (~1 per
+// 8 lookups at C4's shape) instead of 8 B: the bucket round trip drops from 16 to
+// ~9 B per lookup.
+// One (virtual) bin block vb of the probe: keys [vb * NT * PKPT, +NT * PKPT) of the
+// launch (IDS: of its list).  The kernel below loops over them.
+template <int FLAVOR, int LAYOUT, bool STAGE, int KR, int J0, int J1, bool R2, int PKPT, bool IDS, bool E32>
+__device__ __forceinline__ void probe_bin_block(
+    uint32_t vb, const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
+    uint64_t n, const FilterConsts &c, const TileCfg &tc, const TileScratch &sc, uint64_t *__restrict__ buckets,
+    const uint64_t *__restrict__ words, uint8_t *__restrict__ out, const uint32_t *__restrict__ ids) {
     constexpr int NT = kProbeThreads;
-    if (!gate_open(gate)) return;
-    if (IDS) {
-        n = *nlive;  // block-uniform
-        if ((uint64_t)blockIdx.x * (NT * PKPT) >= n) return;
-    }
     extern __shared__ uint32_t lds[];
     const uint32_t T = tc.T, tid = threadIdx.x, k = c.k;
     uint32_t *cnt = lds, *S = lds + T, *GX = lds + 2 * T, *L = lds + 3 * T;
@@ -1596,7 +1696,7 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
     const uint32_t keff = PKPT * ((J1 ? (uint32_t)J1 : k) - J0);  // (probe_keff on the host)
     uint32_t *sidx = lds + probe_sort_offset_words(T);  // [NT * keff] indices, sorted by tile
     uint32_t *skid = sidx + NT * keff;                  // [NT * keff] their keys
-    const uint64_t base = (uint64_t)blockIdx.x * (NT * PKPT);
+    const uint64_t base = (uint64_t)vb * (NT * PKPT);
     BinPhase1<FLAVOR, LAYOUT, PKPT, NT, STAGE, KR, J1, J0, R2, IDS> ph;
     if (R2) ph.gate = out;
     ph.ids = ids;
@@ -1607,12 +1707,24 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
             if (base + (uint64_t)p * NT + tid < n) out[ph.kid[p]] = 1;
     }
     // counts from the placement handles (A_t << kHandleShift | 4 rank, see BinPhase1)
+    if constexpr (E32) {
+        // a touched tile's run is its header word, then its entries
+        for (uint32_t t = tid; t < T; t += NT) {
+            const uint32_t h = (cnt[t] - (lds_addr(cnt + t) << kHandleShift)) >> 2;
+            cnt[t] = h ? h + 1 : 0u;
+        }
+        __syncthreads();
+        probe_bin_tail_e32<NT, PKPT, KR, J0, J1, IDS>(vb, ph, tc, sc, cnt, S, GX, L, wave_sums, sidx,
+                                                      reinterpret_cast<uint32_t *>(buckets), words, out,
+                                                      ids, base, k);
+        return;
+    }
     for (uint32_t t = tid; t < T; t += NT) cnt[t] = (cnt[t] - (lds_addr(cnt + t) << kHandleShift)) >> 2;
     __syncthreads();
     const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
     // reserve a run in every touched tile's bucket shard; GX[t] = its first entry
     // minus the run's local start, L[t] = the first local position past capacity
-    const uint32_t shard = blockIdx.x & (tc.G - 1);
+    const uint32_t shard = vb & (tc.G - 1);
     uint32_t *cur = sc.gcur + (size_t)shard * T;
     for (uint32_t t = tid; t < T; t += NT) {
         const uint32_t h = cnt[t], g = h ? atomicAdd(&cur[t], h) : 0u;
@@ -1644,6 +1756,65 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
             out[kq] = 0;
         }
     }
+}
+
+// A value the compiler must treat as changed here (an empty asm rewrites each 32-bit
+// word in its SGPR): what is computed from it cannot be hoisted out of a loop.
+template <class V>
+__device__ __forceinline__ V launder(const V &v) {
+    static_assert(sizeof(V) % 4 == 0, "whole dwords");
+    uint32_t w[sizeof(V) / 4];
+    __builtin_memcpy(w, (const void *)&v, sizeof(V));
+#pragma unroll
+    for (size_t i = 0; i < sizeof(V) / 4; ++i) asm volatile("" : "+s"(w[i]));
+    V r;
+    __builtin_memcpy((void *)&r, w, sizeof(V));
+    return r;
+}
+#ifndef NB_PROBE_GRID_STRIDE
+#define NB_PROBE_GRID_STRIDE 1
+#endif
+// The probe's bin kernel: a grid-stride loop over the launch's bin blocks (round 6).
+// The grid is capped at kProbeBinBlocksPerCU blocks per CU, a multiple of the G cursor
+// shards, so virtual block vb runs on a block with blockIdx % G == vb % G (its shard's
+// XCD) -- and a launch closed by auto's device-side gate (ProbeGate) dispatches a few
+// thousand blocks instead of one per 1 024 keys.
+template <int FLAVOR, int LAYOUT, bool STAGE, int KR, int J0 = 0, int J1 = 0, bool R2 = false, int PKPT = 1,
+          bool IDS = false, bool E32 = false>
+__global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) void probe_bin_kernel(
+    const uint8_t *__restrict__ keys, const uint64_t *__restrict__ offsets, uint32_t key_len,
+    uint64_t n, FilterConsts c, TileCfg tc, TileScratch sc, uint64_t *__restrict__ buckets,
+    const uint64_t *__restrict__ words, uint8_t *__restrict__ out, ProbeGate gate,
+    const uint32_t *__restrict__ ids, const uint32_t *__restrict__ nlive) {
+    constexpr uint64_t kpb = (uint64_t)kProbeThreads * PKPT;
+    static_assert(!E32 || kpb <= (1 << 11), "E32: kib << ts must stay below bit 31 (ts <= 20)");
+    if (!gate_open(gate)) return;
+    if (IDS) n = *nlive;  // block-uniform
+    const uint64_t nvb = (n + kpb - 1) / kpb;
+#if NB_PROBE_GRID_STRIDE
+    // Blocks take their first bin block by index, the next ones from a counter of
+    // their shard class g = blockIdx % G (bin blocks g, g + G, ...: the shard stays on
+    // the block's XCD), so a short grid finishes together instead of in generations.
+    const uint32_t G = tc.G, g = blockIdx.x & (G - 1), per = gridDim.x / G;
+    extern __shared__ uint32_t lds_next[];
+    uint32_t *next = lds_next + probe_sort_offset_words(tc.T) - 1;  // (a free word before the sort area)
+    for (uint64_t vb = blockIdx.x; vb < nvb;) {
+        // the arguments laundered per iteration: values derived from them are then
+        // recomputed in every block instead of hoisted out of the loop into VGPRs that
+        // stay live across the sort and write-out (+20 VGPRs and spills otherwise)
+        probe_bin_block<FLAVOR, LAYOUT, STAGE, KR, J0, J1, R2, PKPT, IDS, E32>(
+            (uint32_t)vb, launder(keys), launder(offsets), launder(key_len), launder(n), launder(c),
+            launder(tc), launder(sc), launder(buckets), launder(words), launder(out), launder(ids));
+        if (threadIdx.x == 0) *next = per + atomicAdd(&sc.vbctr[g], 1u);
+        __syncthreads();  // (also: the block's LDS reads are done before the next one)
+        vb = g + (uint64_t)G * *next;
+        __syncthreads();  // everyone has read *next
+    }
+#else
+    if (blockIdx.x < nvb)
+        probe_bin_block<FLAVOR, LAYOUT, STAGE, KR, J0, J1, R2, PKPT, IDS, E32>(
+            blockIdx.x, keys, offsets, key_len, n, c, tc, sc, buckets, words, out, ids);
+#endif
 }
 
 // The split probe's survivors of its first round: ids (in the pass) of the keys whose
@@ -1714,6 +1885,7 @@ __global__ __launch_bounds__(NT) void probe_tile_kernel(TileCfg tc, TileScratch 
     extern __shared__ uint32_t tile[];  // [2^ts / 32] filter words, then 2*kShards+1 words
     const uint32_t t = blockIdx.x, tid = threadIdx.x;
     const uint32_t tile_words32 = 1u << (tc.ts - 5), mask = (1u << tc.ts) - 1;
+    if (t == 0 && tid < tc.G && sc.vbctr) sc.vbctr[tid] = 0;  // the bin kernel's counters
     uint32_t *shard_cnt = tile + tile_words32;  // [kShards]
     uint32_t *shard_v0 = shard_cnt + kShards;   // [kShards + 1]
     // the tile's filter words (past the filter's end: zero, never tested)
@@ -1757,6 +1929,113 @@ __global__ __launch_bounds__(NT) void probe_tile_kernel(TileCfg tc, TileScratch 
         for (int u = 0; u < 4; ++u) test(e[u]);
     }
     for (; q < ne; q += NT) test(entry_at(q));
+}
+
+// The tile kernel of E32 buckets (probe_bin_tail_e32): an entry's key comes from the
+// header word that opens its run, so a bucket is read in order.  Each (tile, shard)
+// bucket is one contiguous range: its NT/64/G waves take a contiguous segment each
+// (split at 16-byte boundaries) and stream it in 256-word steps, one 16-byte load per
+// lane; a wave-wide "last header" scan hands every lane the header in force at its
+// first word, and the last header of a step carries into the next.  A segment that
+// starts inside a run finds its header by one backward look (a run is ~9 words at
+// C4's shape; word 0 of every bucket is a header).  kpb = keys per bin block of the
+// launch; IDS: keys are list entries ids[header * kpb + kib] (the split path's second
+// round, with NB_PROBE_ENTRY=32 only).
+// (Measured, not kept: one 4-byte load per lane, so that a miss-store instruction
+// covers 64 consecutive entries instead of 256 -- round one of the split path at 30 %
+// present 597 -> 725 us per 50M-key pass, tools/trace_rounds.py, r06c / r06e; and, in
+// this kernel and probe_tile_kernel, the next step's loads issued before this step's
+// tests and miss stores -- split absent 4.50 -> 4.73 ms, 30 % present 3.68 -> 3.98,
+// profiles/r06f_probe_prefetch_ab.txt.)
+constexpr int kProbeTileUnroll = 4;  // 16-byte loads in flight per lane
+template <int NT = kTileThreads, bool IDS = false>
+__global__ __launch_bounds__(NT) void probe_tile32_kernel(TileCfg tc, TileScratch sc,
+                                                          const uint32_t *__restrict__ buckets,
+                                                          const uint64_t *__restrict__ words,
+                                                          uint64_t nwords, uint8_t *__restrict__ out,
+                                                          ProbeGate gate, uint32_t kpb,
+                                                          const uint32_t *__restrict__ ids) {
+    if (!gate_open(gate)) return;
+    extern __shared__ uint32_t tile[];  // [2^ts / 32] filter words, then kShards counts
+    const uint32_t t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    if (t == 0 && tid < tc.G && sc.vbctr) sc.vbctr[tid] = 0;  // the bin kernel's counters
+    const uint32_t tile_words32 = 1u << (tc.ts - 5), mask = (1u << tc.ts) - 1;
+    uint32_t *shard_cnt = tile + tile_words32;  // [kShards]
+    const uint64_t w0 = (uint64_t)t << (tc.ts - 6);
+    uint64_t *tile64 = reinterpret_cast<uint64_t *>(tile);
+    for (uint32_t w = tid; w < tile_words32 / 2; w += NT)
+        tile64[w] = w0 + w < nwords ? words[w0 + w] : 0ull;
+    if (tid < tc.G) {
+        uint32_t *cp = sc.gcur + (size_t)tid * tc.T + t;
+        shard_cnt[tid] = min(*cp, tc.cap);
+        *cp = 0;  // workspace invariant: cursors are zero between launches
+    }
+    __syncthreads();
+    // (no barrier below: a wave leaves when its segment is done)
+    const uint32_t wps = max(1u, (uint32_t)(NT / 64) / tc.G);  // waves per shard
+    const uint32_t g = wid / wps, part = wid % wps;
+    if (g >= tc.G) return;
+    const uint32_t c = shard_cnt[g];
+    const uint32_t per = ((c + wps - 1) / wps + 3) & ~3u;
+    const uint32_t s0 = min(part * per, c), s1 = min(s0 + per, c);
+    if (s0 >= s1) return;  // wave-uniform
+    const uint32_t *e = buckets + (size_t)bucket_region(tc, t, g) * tc.cap;
+    // header + 1 in force at the current position (0: none seen yet)
+    uint32_t carry = 0;
+    for (uint32_t b = s0; b > 0 && carry == 0; b = b > 64 ? b - 64 : 0) {
+        const bool in = lane < b;
+        const uint32_t w = in ? e[b - 1 - lane] : 0u;
+        const uint64_t hm = __ballot(in && (w >> 31));
+        if (hm) carry = (__shfl(w, (int)__builtin_ctzll(hm)) & 0x7fffffffu) + 1;
+    }
+    auto test = [&](uint32_t w, uint32_t hv) {
+        const uint32_t off = w & mask;
+        if (!((tile[off >> 5] >> (off & 31)) & 1u)) {
+            const uint32_t j = (hv - 1) * kpb + (w >> tc.ts);
+            out[IDS ? ids[j] : j] = 0;
+        }
+    };
+    // one step: the lane's 4 words (the first `valid` of them real), wave-uniform call
+    auto step = [&](const uint4 &v, uint32_t valid) {
+        const uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+        uint32_t last = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if ((uint32_t)i < valid && (ws[i] >> 31)) last = (ws[i] & 0x7fffffffu) + 1;
+        const uint32_t X = wave_last_nonzero(last);
+        const uint32_t prev = __shfl_up(X, 1);
+        uint32_t cur = lane && prev ? prev : carry;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if ((uint32_t)i < valid) {
+                if (ws[i] >> 31) cur = (ws[i] & 0x7fffffffu) + 1;
+                else if (cur) test(ws[i], cur);
+            }
+        }
+        const uint32_t tail = __builtin_amdgcn_readlane(X, 63);
+        if (tail) carry = tail;
+    };
+    constexpr uint32_t kStep = 256, U = kProbeTileUnroll;
+    uint32_t q = s0;
+    for (; q + U * kStep <= s1; q += U * kStep) {
+        uint4 v[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) v[u] = bucket_load(reinterpret_cast<const uint4 *>(e + q + u * kStep) + lane);
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) step(v[u], 4);
+    }
+    for (; q < s1; q += kStep) {
+        const uint32_t p = q + 4 * lane, valid = p < s1 ? min(4u, s1 - p) : 0u;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (valid == 4) {
+            v = bucket_load(reinterpret_cast<const uint4 *>(e + p));
+        } else if (valid) {
+            v.x = e[p];
+            if (valid > 1) v.y = e[p + 1];
+            if (valid > 2) v.z = e[p + 2];
+        }
+        step(v, valid);
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void or_merge_kernel(uint64_t *__restrict__ dst,
@@ -2468,7 +2747,8 @@ int launch_build_f(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
 
 // Probe tiles: the largest 2^ts <= 2^20 (the tile kernel's LDS copy) that still
 // leaves >= 256 tiles; cap per (tile, shard) as the build's.
-TileCfg probe_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
+// E32 buckets also hold one header per run: at most one per bin block and tile.
+TileCfg probe_tiles(uint32_t m, uint64_t n_chunk, uint32_t k, bool e32 = false) {
     TileCfg tc;
     uint32_t ts = 12;
     while (ts < 20 && (((uint64_t)m + (1ull << (ts + 1)) - 1) >> (ts + 1)) >= 256) ++ts;
@@ -2476,7 +2756,8 @@ TileCfg probe_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
     tc.T = (uint32_t)(((uint64_t)m + (1ull << ts) - 1) >> ts);
     tc.G = kShards;
     const double e = (double)n_chunk * k / ((double)tc.T * tc.G);
-    uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0);
+    const uint64_t hdrs = e32 ? ((n_chunk + kProbeThreads - 1) / kProbeThreads + tc.G - 1) / tc.G : 0;
+    uint64_t cap = (uint64_t)(e + 8.0 * std::sqrt(e) + 64.0) + hdrs;
     tc.cap = (uint32_t)std::min<uint64_t>((cap + 7) & ~7ull, 0xFFFFFFC0ull);
     tc.fts = ts;
     tc.mul = tc.fmul = pow2_mul(ts);
@@ -2490,8 +2771,10 @@ TileCfg probe_tiles(uint32_t m, uint64_t n_chunk, uint32_t k) {
 // (163 968 B at k = 12), and those batches take the lane path.
 constexpr size_t kMaxBlockLds = 160 * 1024;
 // keff = entries a thread bins: k for the one-round kernel (probe_keff for a round)
-size_t probe_bin_lds_bytes(uint32_t T, uint32_t keff, bool stage) {
-    size_t sort_bytes = (size_t)2 * kProbeThreads * keff * 4;
+// (E32: a 32-bit word per sort slot, plus a header slot per tile)
+size_t probe_bin_lds_bytes(uint32_t T, uint32_t keff, bool stage, bool e32 = false) {
+    size_t sort_bytes = e32 ? (((size_t)kProbeThreads * keff + T) * 4 + 15) & ~(size_t)15
+                            : (size_t)2 * kProbeThreads * keff * 4;
     if (stage) sort_bytes = std::max<size_t>(sort_bytes, stage_lds_bytes(kProbeThreads));
     return (size_t)probe_sort_offset_words(T) * 4 + sort_bytes;
 }
@@ -2506,7 +2789,10 @@ template <int FLAVOR, int LAYOUT>
 int launch_probe_lane(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                       const FilterConsts &c, const uint64_t *words, uint8_t *out, hipStream_t st,
                       const ProbeGate &gate) {
-    hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, LAYOUT>), dim3(grid_for(n)), dim3(kBlock), 0, st,
+    // (a gated launch, which may be closed, takes a grid of 8 blocks per CU -- full
+    // occupancy for its grid-stride loop -- so that a closed one dispatches little)
+    const uint32_t grid = gate.decide ? std::min<uint32_t>(grid_for(n), 8 * device_cus()) : grid_for(n);
+    hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, LAYOUT>), dim3(grid), dim3(kBlock), 0, st,
                        keys, offsets, key_len, n, c, reinterpret_cast<const uint32_t *>(words), out,
                        gate);
     NB_HIP(hipGetLastError());
@@ -2516,6 +2802,8 @@ int launch_probe_lane(const uint8_t *keys, const uint64_t *offsets, uint32_t key
 // The split tiled probe's first round: each key's first kSplitJ indices.
 constexpr int kSplitJ = 2;
 constexpr int kSplitKPT = 4;  // keys per thread of the split path's first round
+constexpr int kSplitKPT32 = 2;  // the same with E32 entries (a block's keys < 2^11)
+constexpr uint32_t kProbeBinBlocksPerCU = 8;  // grid cap of the probe's bin kernels
 // entries per thread of a probe_bin_kernel launch (its keff)
 constexpr uint32_t probe_keff(uint32_t k, int j0, int j1, int pkpt) {
     return (uint32_t)pkpt * ((j1 ? (uint32_t)j1 : k) - (uint32_t)j0);
@@ -2537,13 +2825,27 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
     int rc;
     if ((rc = get_ws(st, &ws))) return rc;
     std::lock_guard<std::mutex> lk(ws->mu);
-    // chunks whose 64-bit entries stay under ~6 GB of buckets (key ids < 2^32)
+    // E32 (NB_PROBE_ENTRY=32, default): 32-bit entries behind run headers; 64: key << 32 |
+    // offset.  E32 keeps a block's keys below 2^(31 - ts): the split path's first round
+    // then bins two keys per thread instead of four.
+    // E32 entries for the one-round path; the split path keeps 64-bit ones (its first
+    // round at two keys per thread and its second round's list lookups per miss cost
+    // more than the bytes save: 30 % present 3.93 vs 4.82 ms, absent 4.95 vs 5.32 ms,
+    // same box, profiles/r06e_probe_c4.txt).  NB_PROBE_ENTRY: 0 this policy, 32 / 64
+    // either format everywhere.
+    const uint64_t ek = knob(nb::kKnobProbeEntry);
+    const bool e32 = ek == 32 || (ek == 0 && !split);
+    const int kpt1 = e32 ? kSplitKPT32 : kSplitKPT;
+    const uint32_t ebytes = e32 ? 4u : 8u;
+    // chunks whose buckets stay under ~6 GB (entries, headers, answers, with margin:
+    // 10 B per index for 64-bit entries, 6 B for 32-bit ones -- C4's 100M keys in two
+    // passes / one pass) -- key ids < 2^32
     const uint64_t kc = knob(nb::kKnobProbeChunk);
-    const uint64_t budget = std::max<uint64_t>(NT, kc ? std::min<uint64_t>(kc, (6ull << 30) / (10ull * c.k))
-                                                      : (6ull << 30) / (10ull * c.k));
+    const uint64_t cap_keys = (6ull << 30) / ((e32 ? 6ull : 10ull) * c.k);
+    const uint64_t budget = std::max<uint64_t>(NT, kc ? std::min<uint64_t>(kc, cap_keys) : cap_keys);
     const uint64_t passes = (n + budget - 1) / budget;
     const uint64_t chunk = std::max<uint64_t>(1, (n + passes - 1) / passes);
-    const TileCfg tc = probe_tiles(c.fm.m, chunk, c.k);
+    const TileCfg tc = probe_tiles(c.fm.m, chunk, c.k, e32);
     // the split path's second round runs over the compacted list of the first round's
     // survivors -- a count word, then the ids -- kept in the workspace's second bucket
     // array (the two-level build's; unused by the probe) and reserved on every tiled
@@ -2551,33 +2853,65 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
     // capture of auto's gated paths
     const bool compact = c.k > (uint32_t)kSplitJ;
     const size_t ids_bytes = compact ? (chunk + 16) * 4 : 0;
-    if ((rc = ws_reserve(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * 8, &sc, ids_bytes))) return rc;
+    if ((rc = ws_reserve(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * ebytes, &sc, ids_bytes))) return rc;
+    sc.vbctr = super_cursors(*ws);  // (the two-level build's; unused by the probe)
     uint32_t *nlive = compact ? reinterpret_cast<uint32_t *>(ws->buckets2) : nullptr;
     uint32_t *ids = compact ? nlive + 16 : nullptr;
     split = split && c.k > (uint32_t)kSplitJ;
-    const size_t bin_lds = probe_bin_lds_bytes(tc.T, c.k, STAGE);
-    const size_t lds1 = probe_bin_lds_bytes(tc.T, probe_keff(c.k, 0, kSplitJ, kSplitKPT), STAGE);
-    const size_t lds2 = probe_bin_lds_bytes(tc.T, probe_keff(c.k, kSplitJ, 0, 1), STAGE);
+    // the one-round E32 bin kernel takes two keys per thread for 16- / 32-byte keys at
+    // k = 7 (2 048 per block: half the blocks' reservations and fixed costs per key) when
+    // two such blocks fit a CU
+    const uint64_t kptk = knob(nb::kKnobProbeKPT);
+    const bool kpt2 = e32 && !split && c.k == 7 && !STAGE && kptk != 1 &&
+                      (kptk == 2 || probe_bin_lds_bytes(tc.T, probe_keff(c.k, 0, 0, 2), STAGE, true) <= kMaxBlockLds / 2);
+    const size_t bin_lds = probe_bin_lds_bytes(tc.T, probe_keff(c.k, 0, 0, kpt2 ? 2 : 1), STAGE, e32);
+    const size_t lds1 = probe_bin_lds_bytes(tc.T, probe_keff(c.k, 0, kSplitJ, kpt1), STAGE, e32);
+    const size_t lds2 = probe_bin_lds_bytes(tc.T, probe_keff(c.k, kSplitJ, 0, 1), STAGE, e32);
     if (bin_lds > kMaxBlockLds || (split && lds1 > kMaxBlockLds))
         return fail(NB_ERR_UNSUPPORTED, "tiled probe: LDS of the shape");
     const size_t tile_lds = ((size_t)1 << (tc.ts - 3)) + (2 * kShards + 1) * 4;
-    auto bin = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR>;
-    auto bin1 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, kSplitJ, false, kSplitKPT>;
-    auto bin2 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, kSplitJ, 0, true, 1, true>;
+    using BinFn = void (*)(const uint8_t *, const uint64_t *, uint32_t, uint64_t, FilterConsts, TileCfg,
+                           TileScratch, uint64_t *, const uint64_t *, uint8_t *, ProbeGate, const uint32_t *,
+                           const uint32_t *);
+    BinFn bin, bin1, bin2;
+    if (e32) {
+        if (kpt2 && KR == 8 && !STAGE)  // (k = 7 exactly: index loops without k checks, 7 rank registers)
+            bin = probe_bin_kernel<FLAVOR, LAYOUT, false, 7, 0, 7, false, 2, false, true>;
+        else
+            bin = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, 0, false, 1, false, true>;
+        bin1 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, kSplitJ, false, kSplitKPT32, false, true>;
+        bin2 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, kSplitJ, 0, true, 1, true, true>;
+    } else {
+        bin = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR>;
+        bin1 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, kSplitJ, false, kSplitKPT>;
+        bin2 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, kSplitJ, 0, true, 1, true>;
+    }
     auto tile = probe_tile_kernel<kTileThreads>;
+    auto tile32 = probe_tile32_kernel<kTileThreads, false>;
+    auto tile32i = probe_tile32_kernel<kTileThreads, true>;
     if ((rc = allow_lds(bin, bin_lds)) || (split && (rc = allow_lds(bin1, lds1))) ||
-        (split && (rc = allow_lds(bin2, lds2))) || (rc = allow_lds(tile, tile_lds)) ||
+        (split && (rc = allow_lds(bin2, lds2))) ||
+        (rc = e32 ? allow_lds(tile32, tile_lds) : allow_lds(tile, tile_lds)) ||
+        (e32 && split && (rc = allow_lds(tile32i, tile_lds))) ||
         (split && compact && (rc = allow_lds(probe_compact_kernel, kCompactLds))))
         return rc;
     const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
     uint64_t *bk = reinterpret_cast<uint64_t *>(ws->buckets);
+    // the bin kernels loop over their blocks: a grid of kProbeBinBlocksPerCU per CU, a
+    // multiple of the cursor shards (NB_PROBE_BIN_GRID: 0 this cap, else that many per CU)
+    const uint64_t gk = knob(nb::kKnobProbeBinGrid);
+    // -- for a gated launch (auto), which may be closed: an open grid-stride grid costs
+    // ~2 % against one block per 1 024 keys, a closed one-block-per-1 024-keys grid
+    // ~3 ns per block (~0.15 ms per C4 pass)
+    const uint64_t bin_grid_cap = gate.decide ? (uint64_t)device_cus() * (gk ? gk : kProbeBinBlocksPerCU) / tc.G * tc.G
+                                              : (gk ? (uint64_t)device_cus() * gk / tc.G * tc.G : ~0ull);
     for (uint64_t done = 0; done < n; done += chunk) {
         const uint64_t cn = std::min(chunk, n - done);
         const uint8_t *ck = offsets ? keys : keys + done * key_len;
         const uint64_t *co = offsets ? offsets + done : nullptr;
         for (int round = 0; round < (split ? 2 : 1); ++round) {
             auto b = !split ? bin : round == 0 ? bin1 : bin2;
-            const uint64_t kpb = split && round == 0 ? (uint64_t)NT * kSplitKPT : NT;
+            const uint64_t kpb = split && round == 0 ? (uint64_t)NT * kpt1 : kpt2 ? 2ull * NT : NT;
             if (round == 1 && compact) {  // the survivors of round one
                 NB_HIP(hipMemsetAsync(nlive, 0, 4, st));
                 const uint64_t per = (uint64_t)kCompactThreads * kCompactPer;
@@ -2586,39 +2920,55 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
                                    gate);
                 NB_HIP(hipGetLastError());
             }
-            hipLaunchKernelGGL(b, dim3((uint32_t)((cn + kpb - 1) / kpb)), dim3(NT),
+            // (a multiple of the shards: the kernel's block classes, blockIdx % G, are equal)
+            const uint64_t bgrid = (std::min<uint64_t>((cn + kpb - 1) / kpb, bin_grid_cap) + tc.G - 1) / tc.G * tc.G;
+            hipLaunchKernelGGL(b, dim3((uint32_t)bgrid), dim3(NT),
                                !split ? bin_lds : round == 0 ? lds1 : lds2, st, ck, co,
                                key_len, cn, c, tc, sc, bk, words, out + done, gate, ids, nlive);
             NB_HIP(hipGetLastError());
-            hipLaunchKernelGGL(tile, dim3(tc.T), dim3(kTileThreads), tile_lds, st, tc, sc,
-                               (const uint64_t *)bk, words, nwords, out + done, gate);
+            if (!e32)
+                hipLaunchKernelGGL(tile, dim3(tc.T), dim3(kTileThreads), tile_lds, st, tc, sc,
+                                   (const uint64_t *)bk, words, nwords, out + done, gate);
+            else
+                hipLaunchKernelGGL(round == 1 ? tile32i : tile32, dim3(tc.T), dim3(kTileThreads), tile_lds, st,
+                                   tc, sc, (const uint32_t *)bk, words, nwords, out + done, gate, (uint32_t)kpb,
+                                   (const uint32_t *)ids);
             NB_HIP(hipGetLastError());
         }
     }
     return NB_OK;
 }
 
-// The path of a batch probe (NB_PROBE_PATH: 0 auto, 1 lane, 2 tiled): lane for small
-// batches, k > 8 (k > 16 for 32-byte keys) and the non-parity MurmurHash3 flavour;
-// auto probes a sample with the lane kernel first and lets its hit rate pick the
-// path for the rest (ProbeGate), without a host round trip.
+// The path of a batch probe (NB_PROBE_PATH: 0 auto, 1 lane, 2 tiled, 3 split): lane
+// for small batches, k > 8 (k > 16 for 32-byte keys) and the non-parity MurmurHash3
+// flavour; auto probes a sample with the lane kernel first and lets its hit rate pick
+// one of the three paths for the rest (ProbeGate), without a host round trip.
 template <int FLAVOR, int LAYOUT>
 int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
                    const FilterConsts &c, const uint64_t *words, uint8_t *out, hipStream_t st) {
     const uint64_t path = knob(nb::kKnobProbePath);
     constexpr bool kTiledLayout = LAYOUT != kFixedStride && FLAVOR != NB_FLAVOR_MURMUR3_X64_128;
     const uint32_t kmax = LAYOUT == kFixed32 ? 16u : 8u;
+    // (the bin kernels' LDS in both entry formats: auto may launch either)
     const uint32_t pT = probe_tiles(c.fm.m, n, c.k).T;
     const bool tiled_ok = kTiledLayout && c.k <= kmax && pT <= kMaxTiles &&
-                          probe_bin_lds_bytes(pT, c.k, !vec_layout(LAYOUT)) <= kMaxBlockLds;
+                          probe_bin_lds_bytes(pT, c.k, !vec_layout(LAYOUT), false) <= kMaxBlockLds &&
+                          probe_bin_lds_bytes(pT, c.k, !vec_layout(LAYOUT), true) <= kMaxBlockLds;
     const ProbeGate none{nullptr, nullptr, 0, 0, 0};
-    uint32_t pct = (uint32_t)std::min<uint64_t>(knob(nb::kKnobProbeTiledPct), 101);
-    // the split path takes part in auto's choice wherever the tiled path does (k > 2)
+    // the split path takes part in auto's choice wherever the tiled path does (k > 2).
+    // NB_PROBE_TILED_PCT set (non-zero) is honoured as the threshold of the tiled path;
+    // at 0 it is the policy: split_tiled_pct when the split path takes part, else 30.
+    // A split threshold at or above the tiled one leaves the two-way choice.
     constexpr bool kVec = vec_layout(LAYOUT);
-    const uint64_t spk = knob(nb::kKnobProbeSplitPct);
-    const uint32_t split_pct = c.k <= (uint32_t)kSplitJ ? 101u
-                               : spk ? (uint32_t)std::min<uint64_t>(spk, 101) : split_pct_policy(c.k, kVec);
-    if (split_pct <= 100) pct = split_tiled_pct(c.k, kVec);
+    const uint64_t tpk = knob(nb::kKnobProbeTiledPct), spk = knob(nb::kKnobProbeSplitPct);
+    uint32_t pct = tpk ? (uint32_t)std::min<uint64_t>(tpk, 101) : 30u;
+    uint32_t split_pct = c.k <= (uint32_t)kSplitJ ? 101u
+                         : spk ? (uint32_t)std::min<uint64_t>(spk, 101) : split_pct_policy(c.k, kVec);
+    if (split_pct <= 100) {
+        const uint32_t to_tiled = tpk ? pct : split_tiled_pct(c.k, kVec);
+        if (split_pct < to_tiled) pct = to_tiled;
+        else split_pct = 101;
+    }
     if (path == 1 || !tiled_ok || (path == 0 && n < kProbeTiledMin))
         return launch_probe_lane<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, out, st, none);
     auto tiled = [&](const uint8_t *k_, const uint64_t *o_, uint64_t n_, uint8_t *out_,
@@ -2633,11 +2983,13 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
         return fail(NB_ERR_UNSUPPORTED, "tiled probe: unsupported shape");
     };
     if (path == 2 || path == 3) return tiled(keys, offsets, n, out, none, path == 3);
-    // auto: the sample (one key per lane, one count per block).  Outside stream
-    // capture its 16 counts come back to the host (one 64-byte copy and a stream
-    // synchronisation) and only the chosen path is launched; under capture both
-    // paths are launched, gated on the counts on the device -- no host round trip,
-    // but the closed path's blocks still dispatch (~0.3 ms for C4's 98k tiled blocks).
+    // auto: the sample (one key per lane, one count per block), then every path
+    // launched behind it, each gated on the sample's counts on the device (ProbeGate):
+    // the closed paths' blocks return at once, and no host wait (round 6, VERDICT r05
+    // item 6; the bin kernels' capped grids keep a closed launch to a few thousand
+    // blocks).  NB_PROBE_HOST_PICK=1 (outside stream capture only): rounds 3-5's host
+    // read-back instead -- the counts land in host-mapped memory, the host waits for
+    // the sample and launches only the chosen path.
     Workspace *ws;
     int rc;
     if ((rc = get_ws(st, &ws))) return rc;
@@ -2657,15 +3009,16 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
     const uint64_t *ro = offsets ? offsets + S : nullptr;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     NB_HIP(hipStreamIsCapturing(st, &cs));
-    // outside capture the sample's blocks write their counts straight into host-mapped
-    // memory (no copy launch); under capture into device words the gated launches read
-    const ProbeGate sample{cs == hipStreamCaptureStatusNone ? ws->probe_hits_map : ws->probe_hits,
-                           nullptr, kProbeSampleBlocks, (uint32_t)S, 1};
+    const bool host_pick = cs == hipStreamCaptureStatusNone && knob(nb::kKnobProbeHostPick) != 0;
+    // with the host pick the sample's blocks write their counts straight into
+    // host-mapped memory (no copy launch); else into device words the gated launches read
+    const ProbeGate sample{host_pick ? ws->probe_hits_map : ws->probe_hits, nullptr, kProbeSampleBlocks,
+                           (uint32_t)S, 1};
     hipLaunchKernelGGL((bloom_probe_kernel<FLAVOR, LAYOUT>), dim3(kProbeSampleBlocks), dim3(kBlock), 0,
                        st, keys, offsets, key_len, S, c, reinterpret_cast<const uint32_t *>(words),
                        out, sample);
     NB_HIP(hipGetLastError());
-    if (cs == hipStreamCaptureStatusNone) {
+    if (host_pick) {
         NB_HIP(hipEventRecord(ws->ev_probe, st));
         NB_HIP(hipEventSynchronize(ws->ev_probe));
         volatile uint32_t *hs = ws->probe_hits_host;

@@ -26,8 +26,10 @@ constexpr KnobDef kDefs[nb::kKnobCount] = {
     {"NB_BIN_WIDE", 1},      {"NB_SHARDED_STAGE", 0},
     {"NB_OVERLAP", 6},       {"NB_SUBPASSES", 0},
     {"NB_TILE_COUNT", 0},
-    {"NB_PROBE_PATH", 0},    {"NB_PROBE_CHUNK", 0}, {"NB_PROBE_TILED_PCT", 30},
-    {"NB_PROBE_SPLIT_PCT", 0},
+    {"NB_PROBE_PATH", 0},    {"NB_PROBE_CHUNK", 0}, {"NB_PROBE_TILED_PCT", 0},
+    {"NB_PROBE_SPLIT_PCT", 0}, {"NB_PROBE_ENTRY", 0},
+    {"NB_PROBE_BIN_GRID", 0}, {"NB_PROBE_HOST_PICK", 0},
+    {"NB_PROBE_KPT", 0},
     {"NB_FAIL_BUILDS", 0},   {"NB_FAIL_MERKLES", 0},
 };
 

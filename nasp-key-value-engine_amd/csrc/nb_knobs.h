@@ -51,12 +51,30 @@ enum Knob : int {
                         //                   | 3 "split" (the tiled probe in two rounds)
     kKnobProbeChunk,    // NB_PROBE_CHUNK    0: tiled-probe pass policy, else keys per pass
     kKnobProbeTiledPct, // NB_PROBE_TILED_PCT auto: the tiled path from this % of the sample
-                        //                   present (default 30; 50 before round 4's end)
+                        //                   present; 0 (default): the policy -- 65 % (55 %
+                        //                   for k > 8, 40 % for variable-length keys) when
+                        //                   the split path takes part, else 30 %
     kKnobProbeSplitPct, // NB_PROBE_SPLIT_PCT auto, k > 2: the split path from this % present
-                        //                   up to 65 % (55 % for k > 8, 40 % for variable-
-                        //                   length keys), then tiled; 0 (default): the
+                        //                   up to the tiled threshold; 0 (default): the
                         //                   policy, 7 % for 16-/32-byte keys at k <= 8, 18 %
-                        //                   otherwise; > 100: never split
+                        //                   otherwise; > 100, or >= the tiled threshold:
+                        //                   never split (the two-way choice at 30 %)
+    kKnobProbeEntry,    // NB_PROBE_ENTRY    tiled-probe bucket entries: 32 = a 32-bit word
+                        //                   per lookup (key-in-block id | in-tile offset)
+                        //                   behind one header word per run holding the bin
+                        //                   block; 64 = key << 32 | offset (rounds 3-5);
+                        //                   0 (default): 32 for the one-round tiled path,
+                        //                   64 for the split path
+    kKnobProbeBinGrid,  // NB_PROBE_BIN_GRID tiled-probe bin kernels: blocks per CU of their
+                        //                   grid-stride grid (0: the policy, 8)
+    kKnobProbeHostPick, // NB_PROBE_HOST_PICK auto outside stream capture: 0 (default) the
+                        //                   sample's count stays on the device and every
+                        //                   path is launched gated (no host wait); 1: the
+                        //                   host reads the count back and launches only
+                        //                   the chosen path (rounds 3-5)
+    kKnobProbeKPT,      // NB_PROBE_KPT      one-round E32 tiled probe: keys per bin thread
+                        //                   (0 the policy: 2 at k = 7 when two blocks fit a
+                        //                   CU; 1 / 2 force, 2 at k = 7 only)
     kKnobFailBuilds,    // NB_FAIL_BUILDS    fault injection: the next N device builds fail
                         //                   with NB_ERR_HIP before launching anything
     kKnobFailMerkles,   // NB_FAIL_MERKLES   the same for device Merkle trees

@@ -157,7 +157,7 @@ def test_knob_defaults(built):
     """The switches keep their product defaults: the counted-tile policy
     (NB_TILE_COUNT 0), the sub-pass policy (NB_SUBPASSES 0: 2 for multi-pass builds, 1
     for a single pass -- 0 is the policy, not one sub-pass), the tiled probe's pass
-    policy (NB_PROBE_CHUNK 0), auto's tiled threshold (NB_PROBE_TILED_PCT 30) and its
+    policy (NB_PROBE_CHUNK 0), auto's tiled threshold (NB_PROBE_TILED_PCT 0: the policy) and its
     split-path threshold (NB_PROBE_SPLIT_PCT 0: the policy) --
     unless the environment of this process set them.  The switches of the variants
     round 5 removed (measured slower) are refused as unknown names."""
@@ -166,7 +166,7 @@ def test_knob_defaults(built):
         if name not in os.environ:
             assert nbm.get_knob(name) == 0, name
     if "NB_PROBE_TILED_PCT" not in os.environ:
-        assert nbm.get_knob("NB_PROBE_TILED_PCT") == 30
+        assert nbm.get_knob("NB_PROBE_TILED_PCT") == 0
     if "NB_PROBE_SPLIT_PCT" not in os.environ:
         assert nbm.get_knob("NB_PROBE_SPLIT_PCT") == 0
     with nbm.knobs(NB_TILE_COUNT=768):

@@ -89,9 +89,10 @@ def test_buckets_spill(dev, oracle, knobs, m, k, kl, extra):
     np.testing.assert_array_equal(got, oracle.build(0, buf, None, kl, n, m, k, SEED))
 
 
+@pytest.mark.parametrize("entry", [32, 64])
 @pytest.mark.parametrize("path", ["tiled", "split"])
-@pytest.mark.parametrize("chunk", ["0", "1000000"])
-def test_buckets_tiled_probe(dev, oracle, knobs, chunk, path):
+@pytest.mark.parametrize("chunk", ["0", "1000000", "777777"])
+def test_buckets_tiled_probe(dev, oracle, knobs, chunk, path, entry):
     """The tiled probe in key-range passes: a filter of 60 % of 4.5M keys probed
     over all of them, bit-exact; the split path's second round runs each pass over
     that pass's compacted survivors (ids relative to the pass)."""
@@ -105,7 +106,7 @@ def test_buckets_tiled_probe(dev, oracle, knobs, chunk, path):
     nbm.build_device(t_u8(buf, dev), None, kl, npres, m, k, SEED, 0, wt)
     torch.cuda.synchronize()
     words = wt.cpu().numpy().view(np.uint64)
-    knobs(NB_PROBE_PATH=path, NB_PROBE_CHUNK=chunk)
+    knobs(NB_PROBE_PATH=path, NB_PROBE_CHUNK=chunk, NB_PROBE_ENTRY=entry)
     got = dev_probe(dev, buf, None, kl, n, m, k, SEED, words, 0)
     np.testing.assert_array_equal(got, oracle.probe(0, buf, None, kl, n, m, k, SEED, words))
     assert got[:npres].all()

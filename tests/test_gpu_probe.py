@@ -79,12 +79,32 @@ def test_probe_paths_match_oracle(dev, oracle, knobs, probe_shapes, path, shape,
     assert got.mean() - 0.6 < 0.02  # the absent 40 %: false positives only
 
 
+@pytest.mark.parametrize("entry", [32, 64])
 @pytest.mark.parametrize("path", ["tiled", "split"])
-def test_tiled_probe_overflow_and_small_filter(dev, oracle, knobs, path):
+@pytest.mark.parametrize("shape", ["c4_fixed16", "c3_varlen", "c3_varlen_fnv", "c2_fixed16_fnv", "c5_fixed32_k10"])
+def test_probe_entry_formats(dev, oracle, knobs, probe_shapes, path, shape, entry):
+    """Both tiled-probe bucket formats (NB_PROBE_ENTRY): 32-bit entries behind run
+    headers (round 6, the default) and round 3-5's key << 32 | offset words, on every
+    shape of both tiled paths, bit-exact against the oracle; the 32-bit tile kernel's
+    segments start inside runs and find their header by a backward look."""
+    buf, offs, kl, n, m, k, fl = probe_shapes[shape]
+    knobs(NB_PROBE_PATH=path, NB_PROBE_ENTRY=entry)
+    npres = int(n * 0.3)
+    words = device_words(dev, buf, offs, kl, npres, m, k, fl)
+    got = dev_probe(dev, buf, offs, kl, n, m, k, SEED, words, fl)
+    np.testing.assert_array_equal(got, oracle.probe(fl, buf, offs, kl, n, m, k, SEED, words))
+    assert got[:npres].all()
+
+
+@pytest.mark.parametrize("entry", [32, 64])
+@pytest.mark.parametrize("path", ["tiled", "split"])
+def test_tiled_probe_overflow_and_small_filter(dev, oracle, knobs, path, entry):
     """Duplicated keys overflow the probe's buckets (those entries are tested in the
-    bin kernel instead); a small filter (few, small tiles); k = 1 (the split path
-    then runs one round), k = 3 and k = 8."""
-    knobs(NB_PROBE_PATH=path)
+    bin kernel instead; with 32-bit entries a truncated run keeps its header and a run
+    of one key's thousand copies is ~7 000 words long, so segments look back far); a
+    small filter (few, small tiles); k = 1 (the split path then runs one round), k = 3
+    and k = 8."""
+    knobs(NB_PROBE_PATH=path, NB_PROBE_ENTRY=entry)
     from nasp_bloom import synth
     n = 400_000
     dup = np.zeros(n * 16 + 16, np.uint8)

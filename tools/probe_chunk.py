@@ -32,13 +32,18 @@ def main():
     ap.add_argument("--batches", default="present,absent,mixed")
     ap.add_argument("--no-lane", action="store_true")
     ap.add_argument("--split", action="store_true", help="also the split tiled probe (two rounds)")
-    ap.add_argument("--auto-pct", default="", help="auto path at these NB_PROBE_TILED_PCT values")
+    ap.add_argument("--auto-pct", default="", help="auto path at these NB_PROBE_TILED_PCT values ('policy' = 0)")
     ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c3"],
                     help="c4: C4's filter from the 100M probed present keys; c5: C5's shape "
                          "(m = 2^32-1, k = 10, 32-byte keys), --n probed keys, the filter built "
                          "from --fill-keys device-random keys (the present keys among them); c3: "
                          "C3's 100M variable-length keys (8-64 B) and filter, the absent keys "
                          "the same keys with their first byte changed (same offsets)")
+    ap.add_argument("--entries", default="32",
+                    help="tiled / split variants at these NB_PROBE_ENTRY formats (32,64: an A/B)")
+    ap.add_argument("--variant", action="append", default=[],
+                    help="extra variant LABEL:PATH:KNOB=V,KNOB=V (repeatable), e.g. "
+                         "'auto-host:auto:NB_PROBE_HOST_PICK=1'")
     ap.add_argument("--n", type=int, default=50_000_000)
     ap.add_argument("--fill-keys", type=int, default=400_000_000)
     args = ap.parse_args()
@@ -114,10 +119,19 @@ def main():
             nbm.probe_device(b, offs, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out, stream=st)
             torch.cuda.synchronize(dev)
             ref[name] = out.clone()
-    variants = ([] if args.no_lane else [("lane", "lane", 0, "30", {})]) + [
-        (f"tiled C={c / 1e6 if c else 'policy'}M", "tiled", c, "30", {}) for c in map(int, args.chunks.split(",") if args.chunks else [])
-    ] + ([("split", "split", 0, "30", {})] if args.split else []) + [
-        (f"auto pct={p}", "auto", 0, p, {}) for p in filter(None, args.auto_pct.split(","))]
+    ents = [int(e) for e in args.entries.split(",")]
+
+    def ent(e):
+        return "" if len(ents) == 1 else f" e{e}"
+    variants = ([] if args.no_lane else [("lane", "lane", 0, "0", {})]) + [
+        (f"tiled C={c / 1e6 if c else 'policy'}M{ent(e)}", "tiled", c, "0", {"NB_PROBE_ENTRY": e})
+        for c in map(int, args.chunks.split(",") if args.chunks else []) for e in ents
+    ] + ([(f"split{ent(e)}", "split", 0, "0", {"NB_PROBE_ENTRY": e}) for e in ents] if args.split else []) + [
+        (f"auto pct={p}", "auto", 0, "0" if p == "policy" else p, {})
+        for p in filter(None, args.auto_pct.split(","))]
+    for v in args.variant:
+        label, path, kv = (v.split(":", 2) + [""])[:3]
+        variants.append((label, path, 0, "0", {a.split("=")[0]: int(a.split("=")[1]) for a in kv.split(",") if a}))
     table = {}
     bad = 0
     for rep in range(reps):
