@@ -231,6 +231,11 @@ def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=
         mv[:, :3] = kv[:, :3]
         batches.append(("p30", mixed, None))
     res = {}
+    # SURVEY §8(d)'s probe row: keys (and offsets) read once, the filter read once, one
+    # answer byte written per key; traffic from the committed PMC summary of the probe
+    # kernels at the current kernel source (tools/profile_probe.sh), C4 only
+    B = (int(offs[-1].item()) + 8 * (wl.n + 1) if offs is not None else wl.n * key_len) + (wl.m + 7) // 8 + wl.n
+    ppmc = latest_profile("c4_probe", "pmc") if wl.name == "c4_100M_x16B_k7_per_gpu" else None
     for path in ("auto", "lane", "tiled", "split"):
         r = {}
         with nbm.knobs(NB_PROBE_PATH=path):
@@ -238,9 +243,9 @@ def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=
                 with torch.cuda.stream(stream):
                     nbm.probe_device(kk, oo, key_len, wl.n, wl.m, wl.k, seed, flavor, words, out_t,
                                      stream=stream)
-                # wall clock between device synchronisations: the auto path blocks the
-                # host on its sample, so HIP events around the calls would also count the
-                # GPU's clock ramp after each short idle; this counts what a caller sees
+                # wall clock between device synchronisations: what a caller sees (with
+                # NB_PROBE_HOST_PICK=1 the auto path blocks the host on its sample, and
+                # HIP events around the calls would miss that)
                 torch.cuda.synchronize(dev)
                 t0 = time.perf_counter()
                 for _ in range(reps):
@@ -251,11 +256,20 @@ def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=
                 ms = (time.perf_counter() - t0) * 1e3 / reps
                 r[name] = {"value": round(wl.n / (ms * 1e-3) / 1e6, 3), "unit": "Mkeys/s",
                            "ms": round(ms, 4), "positive_rate": round(float(out_t.float().mean()), 6)}
+                pm = ((ppmc or {}).get("paths", {}).get(path, {}).get(name) or {})
+                r[name]["roofline"] = {
+                    "bound": "hbm", "achieved": round(B / (ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(B / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5),
+                    "algorithmic_bytes": B, "traffic": pm.get("hbm_bytes_per_call"),
+                    "device_us": pm.get("device_us_per_call")}
         res[path] = r
-    res["note"] = ("auto = the default (lane kernel on a 4 096-key sample, its hit rate picks lane, "
-                   "split or tiled for the rest); absent keys from another seed; p30 = keys 0-2 of "
-                   "every 10 present, the rest absent; ms = wall clock per call over 5 back-to-back "
-                   "calls between device synchronisations")
+    res["note"] = ("auto = the default (lane kernel on a 4 096-key sample, whose hit count picks lane, "
+                   "split or tiled for the rest on the device: every path launched, the closed ones "
+                   "return at once); absent keys from another seed; p30 = keys 0-2 of every 10 "
+                   "present, the rest absent; ms = wall clock per call over 5 back-to-back calls "
+                   "between device synchronisations; roofline: algorithmic bytes (keys + filter + "
+                   "answers) / ms, traffic and device_us from the committed probe PMC summary ("
+                   + ((ppmc or {}).get("source") or "none at the current kernel source") + ")")
     return res
 
 

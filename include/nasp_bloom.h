@@ -87,8 +87,10 @@ uint64_t nb_device_merkle_count(void);
  * tiled path from this percentage of present keys in its sample; default 0, the policy:
  * the split policy's upper bound above, 30 when auto never splits; a split threshold at
  * or above it leaves the two-way choice), NB_PROBE_ENTRY (tiled-probe bucket entries:
- * 32, default, or 64 bits), NB_PROBE_BIN_GRID (blocks per CU of the tiled-probe bin
- * kernels' grid-stride grid; 0: 8), NB_PROBE_HOST_PICK (1: auto reads its sample back
+ * 32 or 64 bits everywhere; default 0: 32 for the one-round tiled path, 64 for the
+ * split path), NB_PROBE_BIN_GRID (blocks per CU of auto's gated, looping tiled-probe bin
+ * kernels; 0: 2), NB_PROBE_KPT (keys per bin thread of the one-round 32-bit path; 0:
+ * the policy, 2 at k = 7 for 16- / 32-byte keys), NB_PROBE_HOST_PICK (1: auto reads its sample back
  * on the host outside graph capture; 0, default: gated on the device),
  * NB_PACK, NB_TILE_BITS, NB_SHARDS, NB_CHUNK_KEYS, NB_TWO_LEVEL, NB_PACK5,
  * NB_ENTRY32, NB_RANK, NB_FIXED32, NB_FPMOD, NB_KEXACT, NB_BIN_WIDE, NB_OVERLAP (two-level
@@ -238,9 +240,9 @@ int nb_build_device_ex(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_
  * there (NB_PROBE_SPLIT_PCT > 100: the tiled path from 30 %).  The choice is made on
  * the device: every path is launched behind the sample and gated on its count, so
  * auto never waits on the host (NB_PROBE_HOST_PICK=1 restores rounds 3-5's host
- * read-back outside graph capture).  The tiled paths' bucket entries are 32-bit words
- * behind one header word per run (NB_PROBE_ENTRY=64: key << 32 | offset).  Same
- * answers on every path. */
+ * read-back outside graph capture).  The one-round tiled path's bucket entries are
+ * 32-bit words behind one header word per run, the split path's key << 32 | offset
+ * (NB_PROBE_ENTRY).  Same answers on every path. */
 int nb_probe_device(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_t key_len,
                     uint64_t n, uint32_t m, uint32_t k, uint64_t h2_seed, int flavor,
                     const uint64_t *d_words, uint8_t *d_out, void *stream);

@@ -279,10 +279,20 @@ __host__ __device__ inline uint32_t probe_pick(uint64_t h, uint64_t s, uint32_t 
     if (split_pct <= 100 && 100 * h >= (uint64_t)split_pct * s) return 3u;
     return 1u;
 }
+// The counts are read with device-scope atomic loads: coherent with the sample
+// kernel's stores whatever a CU's caches hold from an earlier call.  (Round 6: plain
+// loads became scalar loads, and in replays of a captured graph some kernels of one
+// call decided on the previous replay's counts -- a tiled bin kernel open behind a
+// closed tile kernel left its cursors for the split path's buckets, whose tile kernel
+// then read another layout's words as key ids: a memory fault,
+// tools/diag_graph_auto.py.)
+__device__ __forceinline__ uint32_t coherent_load(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 __device__ __forceinline__ bool gate_open(const ProbeGate &g) {
     if (!g.decide) return true;
-    uint32_t h = 0;  // uniform: scalar loads
-    for (uint32_t b = 0; b < g.blocks; ++b) h += g.decide[b];
+    uint32_t h = 0;
+    for (uint32_t b = 0; b < g.blocks; ++b) h += coherent_load(g.decide + b);
     return probe_pick(h, g.sample, g.pct, g.split_pct) == g.want;
 }
 
@@ -551,6 +561,8 @@ struct TileScratch {
     uint32_t *vbctr = nullptr;  // tiled probe: [G] bin-block counters of the grid-stride
                                 // bin kernels (zero between launches: the tile kernel
                                 // after each bin kernel resets them)
+    uint32_t *nlive = nullptr;  // split probe: the survivor count, zeroed by the tile
+                                // kernels ahead of the compaction (no memset node)
 };
 
 // Phases 2-4 of the bin kernel in rank mode when T <= 2 NT: thread tid owns the
@@ -1455,7 +1467,7 @@ __global__ __launch_bounds__(NT) void bloom_tile_or_kernel(
     for (uint32_t w = tid; w < 2 * nw64; w += NT) tile[w] = 0;
     if (tid < tc.G) {
         uint32_t *cp = sc.gcur + (size_t)tid * tc.T + t;
-        shard_cnt[tid] = min(*cp, tc.cap);
+        shard_cnt[tid] = min(coherent_load(cp), tc.cap);  // (written by another kernel's atomics)
         *cp = 0;  // workspace invariant: cursors are zero between builds
     }
     __syncthreads();
@@ -1615,6 +1627,10 @@ __device__ __forceinline__ void probe_bin_tail_e32(uint32_t vb, const PH &ph, co
         }
     }
     __syncthreads();
+    // write-out: each wave one contiguous range of slots, 64 at a time (one slot per
+    // lane: a store instruction covers ~7 runs.  Four slots per lane -- one 16-byte LDS
+    // read and one tile scan per 256 slots -- measured slower, 0.87 -> 1.02 ms per 50M
+    // keys: each store instruction then spans ~28 runs, profiles/r06r_probe_trace.txt)
     constexpr uint32_t kW = NT / 64;
     const uint32_t per = (total + kW - 1) / kW;
     const uint32_t s0 = min(wid * per, total), s1 = min(s0 + per, total);
@@ -1771,14 +1787,8 @@ __device__ __forceinline__ V launder(const V &v) {
     __builtin_memcpy((void *)&r, w, sizeof(V));
     return r;
 }
-#ifndef NB_PROBE_GRID_STRIDE
-#define NB_PROBE_GRID_STRIDE 1
-#endif
-// The probe's bin kernel: a grid-stride loop over the launch's bin blocks (round 6).
-// The grid is capped at kProbeBinBlocksPerCU blocks per CU, a multiple of the G cursor
-// shards, so virtual block vb runs on a block with blockIdx % G == vb % G (its shard's
-// XCD) -- and a launch closed by auto's device-side gate (ProbeGate) dispatches a few
-// thousand blocks instead of one per 1 024 keys.
+constexpr uint32_t kVbClasses = 64;  // bin-block counter classes of the probe's bin kernels
+// The probe's bin kernel: one bin block (NT x PKPT keys) per workgroup.
 template <int FLAVOR, int LAYOUT, bool STAGE, int KR, int J0 = 0, int J1 = 0, bool R2 = false, int PKPT = 1,
           bool IDS = false, bool E32 = false>
 __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) void probe_bin_kernel(
@@ -1789,32 +1799,84 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
     constexpr uint64_t kpb = (uint64_t)kProbeThreads * PKPT;
     static_assert(!E32 || kpb <= (1 << 11), "E32: kib << ts must stay below bit 31 (ts <= 20)");
     if (!gate_open(gate)) return;
-    if (IDS) n = *nlive;  // block-uniform
-    const uint64_t nvb = (n + kpb - 1) / kpb;
-#if NB_PROBE_GRID_STRIDE
-    // Blocks take their first bin block by index, the next ones from a counter of
-    // their shard class g = blockIdx % G (bin blocks g, g + G, ...: the shard stays on
-    // the block's XCD), so a short grid finishes together instead of in generations.
-    const uint32_t G = tc.G, g = blockIdx.x & (G - 1), per = gridDim.x / G;
-    extern __shared__ uint32_t lds_next[];
-    uint32_t *next = lds_next + probe_sort_offset_words(tc.T) - 1;  // (a free word before the sort area)
-    for (uint64_t vb = blockIdx.x; vb < nvb;) {
-        // the arguments laundered per iteration: values derived from them are then
-        // recomputed in every block instead of hoisted out of the loop into VGPRs that
-        // stay live across the sort and write-out (+20 VGPRs and spills otherwise)
-        probe_bin_block<FLAVOR, LAYOUT, STAGE, KR, J0, J1, R2, PKPT, IDS, E32>(
-            (uint32_t)vb, launder(keys), launder(offsets), launder(key_len), launder(n), launder(c),
-            launder(tc), launder(sc), launder(buckets), launder(words), launder(out), launder(ids));
-        if (threadIdx.x == 0) *next = per + atomicAdd(&sc.vbctr[g], 1u);
-        __syncthreads();  // (also: the block's LDS reads are done before the next one)
-        vb = g + (uint64_t)G * *next;
-        __syncthreads();  // everyone has read *next
-    }
-#else
-    if (blockIdx.x < nvb)
+    if (IDS) n = min<uint64_t>(__builtin_amdgcn_readfirstlane(coherent_load(nlive)), n);  // <= the list's capacity
+    if (blockIdx.x < (n + kpb - 1) / kpb)
         probe_bin_block<FLAVOR, LAYOUT, STAGE, KR, J0, J1, R2, PKPT, IDS, E32>(
             blockIdx.x, keys, offsets, key_len, n, c, tc, sc, buckets, words, out, ids);
+}
+
+// The same kernel looping over the bin blocks (round 6, auto's gated launches, which
+// may be closed): a grid of kProbeBinBlocksPerCU per CU, so a closed launch dispatches
+// a few thousand workgroups instead of one per bin block.  Its only argument is this
+// struct, and every iteration reads it afresh from the kernel-argument segment
+// through a laundered pointer: a loop over the plain kernel's arguments kept them and
+// what is derived from them live across iterations (~70 SGPRs spilled to VGPR lanes,
+// the open kernel ~15 % slower than one workgroup per bin block).
+struct ProbeBinArgs {
+    const uint8_t *keys;
+    const uint64_t *offsets;
+    uint64_t n;
+    uint8_t *out;
+    uint64_t *buckets;
+    const uint64_t *words;
+    const uint32_t *ids;
+    const uint32_t *nlive;
+    uint32_t key_len;
+    uint32_t pad_;
+    FilterConsts c;
+    TileCfg tc;
+    TileScratch sc;
+    ProbeGate gate;
+};
+// A kernel's single struct argument, read afresh from the kernel-argument segment
+// through a laundered pointer (scalar loads; nothing of it stays live across a loop).
+template <class A>
+__device__ __forceinline__ A reload_kernel_args() {
+#if defined(__HIP_DEVICE_COMPILE__)
+    typedef const __attribute__((address_space(4))) A *KArgs;
+    const KArgs ap = launder((KArgs)__builtin_amdgcn_kernarg_segment_ptr());
+    return *ap;
+#else
+    return A{};  // (host pass only; never runs)
 #endif
+}
+template <int FLAVOR, int LAYOUT, bool STAGE, int KR, int J0 = 0, int J1 = 0, bool R2 = false, int PKPT = 1,
+          bool IDS = false, bool E32 = false>
+__global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) void probe_bin_loop_kernel(
+    ProbeBinArgs a) {
+    constexpr uint64_t kpb = (uint64_t)kProbeThreads * PKPT;
+    static_assert(!E32 || kpb <= (1 << 11), "E32: kib << ts must stay below bit 31 (ts <= 20)");
+    if (!gate_open(a.gate)) return;
+    uint64_t n = a.n;
+    if (IDS) n = min<uint64_t>(__builtin_amdgcn_readfirstlane(coherent_load(a.nlive)), n);  // <= the list's capacity
+    const uint64_t nvb = (n + kpb - 1) / kpb;
+    // Blocks take their first bin block by index.  A grid that covers every bin block
+    // stops there; a capped one takes the next ones from kVbClasses counters, class
+    // c = blockIdx % kVbClasses handing out bin blocks c, c + kVbClasses, ... (a
+    // multiple of the G shards: a bin block's shard stays on its workgroup's XCD; 64
+    // classes keep the counters' atomics from queueing on a few addresses), so a short
+    // grid finishes together instead of in generations.
+    const uint32_t c_ = blockIdx.x & (kVbClasses - 1), per = gridDim.x / kVbClasses;
+    uint32_t *const vbctr = a.sc.vbctr;
+    extern __shared__ uint32_t lds_next[];
+    uint32_t *next = lds_next + probe_sort_offset_words(a.tc.T) - 1;  // (a free word before the sort area)
+    const bool fetch = gridDim.x < nvb;  // uniform
+    for (uint64_t vb = blockIdx.x; vb < nvb;) {
+        // the next bin block's counter fetch goes out before this one's work (its round
+        // trip is hidden behind it)
+        uint32_t pre = 0;
+        if (fetch && threadIdx.x == 0) pre = atomicAdd(&vbctr[c_], 1u);
+        {
+            const ProbeBinArgs b = reload_kernel_args<ProbeBinArgs>();
+            probe_bin_block<FLAVOR, LAYOUT, STAGE, KR, J0, J1, R2, PKPT, IDS, E32>(
+                (uint32_t)vb, b.keys, b.offsets, b.key_len, n, b.c, b.tc, b.sc, b.buckets, b.words, b.out, b.ids);
+        }
+        if (!fetch) break;
+        if (threadIdx.x == 0) *next = per + pre;
+        __syncthreads();  // (also: the block's LDS reads are done before the next one)
+        vb = c_ + (uint64_t)kVbClasses * *next;
+        __syncthreads();  // everyone has read *next
+    }
 }
 
 // The split probe's survivors of its first round: ids (in the pass) of the keys whose
@@ -1827,6 +1889,8 @@ __global__ __launch_bounds__(kProbeThreads, NB_BIN_MIN_WAVES(kProbeThreads)) voi
 // lane's own 16 stores would each hit a different line.
 constexpr int kCompactThreads = 1024, kCompactPer = 16;
 constexpr size_t kCompactLds = ((size_t)kCompactThreads * kCompactPer + kCompactThreads / 64 + 2) * 4;
+// (a grid-stride loop over the 16 384-answer chunks: auto's gated launches, which may
+// be closed, take a short grid)
 __global__ __launch_bounds__(kCompactThreads) void probe_compact_kernel(const uint8_t *__restrict__ ans,
                                                                          uint32_t n, uint32_t *__restrict__ ids,
                                                                          uint32_t *__restrict__ nlive,
@@ -1835,57 +1899,66 @@ __global__ __launch_bounds__(kCompactThreads) void probe_compact_kernel(const ui
     extern __shared__ uint32_t stage[];  // [NT * 16] the block's ids, then the wave sums
     uint32_t *wsum = stage + kCompactThreads * kCompactPer;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t i0 = (blockIdx.x * kCompactThreads + tid) * kCompactPer;
-    uint32_t live = 0;
-    if ((reinterpret_cast<uintptr_t>(ans) & 3) == 0 && i0 + kCompactPer <= n) {  // (kernel-uniform alignment)
-        const uint32_t *a4 = reinterpret_cast<const uint32_t *>(ans + i0);
+    constexpr uint32_t kChunk = kCompactThreads * kCompactPer;
+    const uint32_t nchunks = (n + kChunk - 1) / kChunk;
+    for (uint32_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+        if (ch != blockIdx.x) __syncthreads();  // the previous chunk's ids are out
+        const uint32_t i0 = ch * kChunk + tid * kCompactPer;
+        uint32_t live = 0;
+        if ((reinterpret_cast<uintptr_t>(ans) & 3) == 0 && i0 + kCompactPer <= n) {  // (kernel-uniform alignment)
+            const uint32_t *a4 = reinterpret_cast<const uint32_t *>(ans + i0);
 #pragma unroll
-        for (int w = 0; w < kCompactPer / 4; ++w) {
-            const uint32_t v = a4[w];
+            for (int w = 0; w < kCompactPer / 4; ++w) {
+                const uint32_t v = a4[w];
 #pragma unroll
-            for (int b = 0; b < 4; ++b)
-                if ((v >> (8 * b)) & 0xffu) live |= 1u << (4 * w + b);
+                for (int b = 0; b < 4; ++b)
+                    if ((v >> (8 * b)) & 0xffu) live |= 1u << (4 * w + b);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < kCompactPer; ++q)
+                if (i0 + q < n && ans[i0 + q]) live |= 1u << q;
         }
-    } else {
-#pragma unroll
-        for (int q = 0; q < kCompactPer; ++q)
-            if (i0 + q < n && ans[i0 + q]) live |= 1u << q;
-    }
-    const uint32_t cnt = __popc(live), incl = wave_inclusive_scan(cnt);
-    if (lane == 63) wsum[wid] = incl;
-    __syncthreads();
-    if (wid == 0) {
-        constexpr uint32_t kW = kCompactThreads / 64;
-        const uint32_t w = lane < kW ? wsum[lane] : 0u, wi = wave_inclusive_scan(w);
-        if (lane < kW) wsum[lane] = wi - w;
-        if (lane == kW - 1) {
-            wsum[kW] = wi;
-            wsum[kW + 1] = wi ? atomicAdd(nlive, wi) : 0u;
+        const uint32_t cnt = __popc(live), incl = wave_inclusive_scan(cnt);
+        if (lane == 63) wsum[wid] = incl;
+        __syncthreads();
+        if (wid == 0) {
+            constexpr uint32_t kW = kCompactThreads / 64;
+            const uint32_t w = lane < kW ? wsum[lane] : 0u, wi = wave_inclusive_scan(w);
+            if (lane < kW) wsum[lane] = wi - w;
+            if (lane == kW - 1) {
+                wsum[kW] = wi;
+                wsum[kW + 1] = wi ? atomicAdd(nlive, wi) : 0u;
+            }
         }
+        __syncthreads();
+        uint32_t o = wsum[wid] + incl - cnt;  // in the block
+        while (live) {
+            const uint32_t q = __builtin_ctz(live);
+            live &= live - 1;
+            stage[o++] = i0 + q;
+        }
+        __syncthreads();
+        const uint32_t total = wsum[kCompactThreads / 64], gb = wsum[kCompactThreads / 64 + 1];
+        for (uint32_t j = tid; j < total; j += kCompactThreads)
+            if (gb + j < n) ids[gb + j] = stage[j];  // (the list holds n ids: a guard, never taken)
     }
-    __syncthreads();
-    uint32_t o = wsum[wid] + incl - cnt;  // in the block
-    while (live) {
-        const uint32_t q = __builtin_ctz(live);
-        live &= live - 1;
-        stage[o++] = i0 + q;
-    }
-    __syncthreads();
-    const uint32_t total = wsum[kCompactThreads / 64], gb = wsum[kCompactThreads / 64 + 1];
-    for (uint32_t j = tid; j < total; j += kCompactThreads) ids[gb + j] = stage[j];
 }
 
+// (n: the pass's keys -- an entry's key is checked against it before its answer is
+// stored, so no bucket content can address memory outside the answers)
 template <int NT = kTileThreads>
 __global__ __launch_bounds__(NT) void probe_tile_kernel(TileCfg tc, TileScratch sc,
                                                         const uint64_t *__restrict__ buckets,
                                                         const uint64_t *__restrict__ words,
                                                         uint64_t nwords, uint8_t *__restrict__ out,
-                                                        ProbeGate gate) {
+                                                        ProbeGate gate, uint32_t n) {
     if (!gate_open(gate)) return;
     extern __shared__ uint32_t tile[];  // [2^ts / 32] filter words, then 2*kShards+1 words
     const uint32_t t = blockIdx.x, tid = threadIdx.x;
     const uint32_t tile_words32 = 1u << (tc.ts - 5), mask = (1u << tc.ts) - 1;
-    if (t == 0 && tid < tc.G && sc.vbctr) sc.vbctr[tid] = 0;  // the bin kernel's counters
+    if (t == 0 && tid < kVbClasses && sc.vbctr) sc.vbctr[tid] = 0;  // the bin kernel's counters
+    if (t == 0 && tid == 0 && sc.nlive) *sc.nlive = 0;        // the next compaction's count
     uint32_t *shard_cnt = tile + tile_words32;  // [kShards]
     uint32_t *shard_v0 = shard_cnt + kShards;   // [kShards + 1]
     // the tile's filter words (past the filter's end: zero, never tested)
@@ -1895,7 +1968,7 @@ __global__ __launch_bounds__(NT) void probe_tile_kernel(TileCfg tc, TileScratch 
         tile64[w] = w0 + w < nwords ? words[w0 + w] : 0ull;
     if (tid < tc.G) {
         uint32_t *cp = sc.gcur + (size_t)tid * tc.T + t;
-        shard_cnt[tid] = min(*cp, tc.cap);
+        shard_cnt[tid] = min(coherent_load(cp), tc.cap);  // (written by another kernel's atomics)
         *cp = 0;  // workspace invariant: cursors are zero between launches
     }
     __syncthreads();
@@ -1910,8 +1983,8 @@ __global__ __launch_bounds__(NT) void probe_tile_kernel(TileCfg tc, TileScratch 
     __syncthreads();
     const uint32_t ne = shard_v0[tc.G];
     auto test = [&](uint64_t e) {
-        const uint32_t off = (uint32_t)e & mask;
-        if (!((tile[off >> 5] >> (off & 31)) & 1u)) out[(uint32_t)(e >> 32)] = 0;
+        const uint32_t off = (uint32_t)e & mask, kid = (uint32_t)(e >> 32);
+        if (!((tile[off >> 5] >> (off & 31)) & 1u) && kid < n) out[kid] = 0;
     };
     // the G shards as one flat range of entries; a lane's entry indices only grow,
     // so its shard index is advanced, never searched
@@ -1954,11 +2027,12 @@ __global__ __launch_bounds__(NT) void probe_tile32_kernel(TileCfg tc, TileScratc
                                                           const uint64_t *__restrict__ words,
                                                           uint64_t nwords, uint8_t *__restrict__ out,
                                                           ProbeGate gate, uint32_t kpb,
-                                                          const uint32_t *__restrict__ ids) {
+                                                          const uint32_t *__restrict__ ids, uint32_t n) {
     if (!gate_open(gate)) return;
     extern __shared__ uint32_t tile[];  // [2^ts / 32] filter words, then kShards counts
     const uint32_t t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    if (t == 0 && tid < tc.G && sc.vbctr) sc.vbctr[tid] = 0;  // the bin kernel's counters
+    if (t == 0 && tid < kVbClasses && sc.vbctr) sc.vbctr[tid] = 0;  // the bin kernel's counters
+    if (t == 0 && tid == 0 && sc.nlive) *sc.nlive = 0;        // the next compaction's count
     const uint32_t tile_words32 = 1u << (tc.ts - 5), mask = (1u << tc.ts) - 1;
     uint32_t *shard_cnt = tile + tile_words32;  // [kShards]
     const uint64_t w0 = (uint64_t)t << (tc.ts - 6);
@@ -1967,7 +2041,7 @@ __global__ __launch_bounds__(NT) void probe_tile32_kernel(TileCfg tc, TileScratc
         tile64[w] = w0 + w < nwords ? words[w0 + w] : 0ull;
     if (tid < tc.G) {
         uint32_t *cp = sc.gcur + (size_t)tid * tc.T + t;
-        shard_cnt[tid] = min(*cp, tc.cap);
+        shard_cnt[tid] = min(coherent_load(cp), tc.cap);  // (written by another kernel's atomics)
         *cp = 0;  // workspace invariant: cursors are zero between launches
     }
     __syncthreads();
@@ -1991,8 +2065,11 @@ __global__ __launch_bounds__(NT) void probe_tile32_kernel(TileCfg tc, TileScratc
     auto test = [&](uint32_t w, uint32_t hv) {
         const uint32_t off = w & mask;
         if (!((tile[off >> 5] >> (off & 31)) & 1u)) {
-            const uint32_t j = (hv - 1) * kpb + (w >> tc.ts);
-            out[IDS ? ids[j] : j] = 0;
+            const uint32_t j = (hv - 1) * kpb + (w >> tc.ts);  // (n: a guard, as probe_tile_kernel)
+            if (j < n) {
+                const uint32_t kid = IDS ? ids[j] : j;
+                if (kid < n) out[kid] = 0;
+            }
         }
     };
     // one step: the lane's 4 words (the first `valid` of them real), wave-uniform call
@@ -2803,7 +2880,7 @@ int launch_probe_lane(const uint8_t *keys, const uint64_t *offsets, uint32_t key
 constexpr int kSplitJ = 2;
 constexpr int kSplitKPT = 4;  // keys per thread of the split path's first round
 constexpr int kSplitKPT32 = 2;  // the same with E32 entries (a block's keys < 2^11)
-constexpr uint32_t kProbeBinBlocksPerCU = 8;  // grid cap of the probe's bin kernels
+constexpr uint32_t kProbeBinBlocksPerCU = 2;  // grid of the probe's looping bin kernels (two resident)
 // entries per thread of a probe_bin_kernel launch (its keff)
 constexpr uint32_t probe_keff(uint32_t k, int j0, int j1, int pkpt) {
     return (uint32_t)pkpt * ((j1 ? (uint32_t)j1 : k) - (uint32_t)j0);
@@ -2838,14 +2915,16 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
     const int kpt1 = e32 ? kSplitKPT32 : kSplitKPT;
     const uint32_t ebytes = e32 ? 4u : 8u;
     // chunks whose buckets stay under ~6 GB (entries, headers, answers, with margin:
-    // 10 B per index for 64-bit entries, 6 B for 32-bit ones -- C4's 100M keys in two
-    // passes / one pass) -- key ids < 2^32
+    // 10 B per index for 64-bit entries, 6 B for 32-bit ones; the split path's rounds
+    // bin max(2, k - 2) indices of a key -- C4's 100M keys in one pass either way) --
+    // key ids < 2^32
     const uint64_t kc = knob(nb::kKnobProbeChunk);
-    const uint64_t cap_keys = (6ull << 30) / ((e32 ? 6ull : 10ull) * c.k);
+    const uint64_t kidx = split && c.k > (uint32_t)kSplitJ ? std::max<uint32_t>(kSplitJ, c.k - kSplitJ) : c.k;
+    const uint64_t cap_keys = (6ull << 30) / ((e32 ? 6ull : 10ull) * kidx);
     const uint64_t budget = std::max<uint64_t>(NT, kc ? std::min<uint64_t>(kc, cap_keys) : cap_keys);
     const uint64_t passes = (n + budget - 1) / budget;
     const uint64_t chunk = std::max<uint64_t>(1, (n + passes - 1) / passes);
-    const TileCfg tc = probe_tiles(c.fm.m, chunk, c.k, e32);
+    const TileCfg tc = probe_tiles(c.fm.m, chunk, (uint32_t)kidx, e32);  // (capacity: a round's indices)
     // the split path's second round runs over the compacted list of the first round's
     // survivors -- a count word, then the ids -- kept in the workspace's second bucket
     // array (the two-level build's; unused by the probe) and reserved on every tiled
@@ -2856,6 +2935,7 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
     if ((rc = ws_reserve(*ws, c.fm.m, (size_t)tc.T * tc.G * tc.cap * ebytes, &sc, ids_bytes))) return rc;
     sc.vbctr = super_cursors(*ws);  // (the two-level build's; unused by the probe)
     uint32_t *nlive = compact ? reinterpret_cast<uint32_t *>(ws->buckets2) : nullptr;
+    sc.nlive = nlive;
     uint32_t *ids = compact ? nlive + 16 : nullptr;
     split = split && c.k > (uint32_t)kSplitJ;
     // the one-round E32 bin kernel takes two keys per thread for 16- / 32-byte keys at
@@ -2873,38 +2953,51 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
     using BinFn = void (*)(const uint8_t *, const uint64_t *, uint32_t, uint64_t, FilterConsts, TileCfg,
                            TileScratch, uint64_t *, const uint64_t *, uint8_t *, ProbeGate, const uint32_t *,
                            const uint32_t *);
+    // gated launches (auto; possibly closed) take the looping bin kernels on a capped
+    // grid; the forced-format variants (NB_PROBE_ENTRY=32 split, =64 one-round) exist
+    // without the loop only
+    const bool loop = gate.decide != nullptr;
+    using LoopFn = void (*)(ProbeBinArgs);
     BinFn bin, bin1, bin2;
+    LoopFn lbin = nullptr, lbin1 = nullptr, lbin2 = nullptr;
     if (e32) {
-        if (kpt2 && KR == 8 && !STAGE)  // (k = 7 exactly: index loops without k checks, 7 rank registers)
+        if (kpt2 && KR == 8 && !STAGE) {  // (k = 7 exactly: index loops without k checks, 7 rank registers)
             bin = probe_bin_kernel<FLAVOR, LAYOUT, false, 7, 0, 7, false, 2, false, true>;
-        else
+            lbin = probe_bin_loop_kernel<FLAVOR, LAYOUT, false, 7, 0, 7, false, 2, false, true>;
+        } else {
             bin = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, 0, false, 1, false, true>;
+            lbin = probe_bin_loop_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, 0, false, 1, false, true>;
+        }
         bin1 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, kSplitJ, false, kSplitKPT32, false, true>;
         bin2 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, kSplitJ, 0, true, 1, true, true>;
     } else {
         bin = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR>;
         bin1 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, kSplitJ, false, kSplitKPT>;
         bin2 = probe_bin_kernel<FLAVOR, LAYOUT, STAGE, KR, kSplitJ, 0, true, 1, true>;
+        lbin1 = probe_bin_loop_kernel<FLAVOR, LAYOUT, STAGE, KR, 0, kSplitJ, false, kSplitKPT>;
+        lbin2 = probe_bin_loop_kernel<FLAVOR, LAYOUT, STAGE, KR, kSplitJ, 0, true, 1, true>;
     }
+    const bool looping = loop && (split ? lbin1 != nullptr : lbin != nullptr);
     auto tile = probe_tile_kernel<kTileThreads>;
     auto tile32 = probe_tile32_kernel<kTileThreads, false>;
     auto tile32i = probe_tile32_kernel<kTileThreads, true>;
     if ((rc = allow_lds(bin, bin_lds)) || (split && (rc = allow_lds(bin1, lds1))) ||
-        (split && (rc = allow_lds(bin2, lds2))) ||
+        (split && (rc = allow_lds(bin2, lds2))) || (lbin && (rc = allow_lds(lbin, bin_lds))) ||
+        (split && lbin1 && (rc = allow_lds(lbin1, lds1))) || (split && lbin2 && (rc = allow_lds(lbin2, lds2))) ||
         (rc = e32 ? allow_lds(tile32, tile_lds) : allow_lds(tile, tile_lds)) ||
         (e32 && split && (rc = allow_lds(tile32i, tile_lds))) ||
         (split && compact && (rc = allow_lds(probe_compact_kernel, kCompactLds))))
         return rc;
     const uint64_t nwords = ((uint64_t)c.fm.m + 63) / 64;
     uint64_t *bk = reinterpret_cast<uint64_t *>(ws->buckets);
-    // the bin kernels loop over their blocks: a grid of kProbeBinBlocksPerCU per CU, a
-    // multiple of the cursor shards (NB_PROBE_BIN_GRID: 0 this cap, else that many per CU)
+    // the looping bin kernels (gated launches) run a grid of kProbeBinBlocksPerCU per CU
+    // (NB_PROBE_BIN_GRID: that many instead), a multiple of their kVbClasses counter
+    // classes; every other launch one workgroup per bin block
     const uint64_t gk = knob(nb::kKnobProbeBinGrid);
-    // -- for a gated launch (auto), which may be closed: an open grid-stride grid costs
-    // ~2 % against one block per 1 024 keys, a closed one-block-per-1 024-keys grid
-    // ~3 ns per block (~0.15 ms per C4 pass)
-    const uint64_t bin_grid_cap = gate.decide ? (uint64_t)device_cus() * (gk ? gk : kProbeBinBlocksPerCU) / tc.G * tc.G
-                                              : (gk ? (uint64_t)device_cus() * gk / tc.G * tc.G : ~0ull);
+    const uint64_t bin_grid_cap =
+        looping ? std::max<uint64_t>(kVbClasses, (uint64_t)device_cus() * (gk ? gk : kProbeBinBlocksPerCU) /
+                                                     kVbClasses * kVbClasses)
+                : ~0ull;
     for (uint64_t done = 0; done < n; done += chunk) {
         const uint64_t cn = std::min(chunk, n - done);
         const uint8_t *ck = offsets ? keys : keys + done * key_len;
@@ -2912,27 +3005,34 @@ int launch_probe_tiled(const uint8_t *keys, const uint64_t *offsets, uint32_t ke
         for (int round = 0; round < (split ? 2 : 1); ++round) {
             auto b = !split ? bin : round == 0 ? bin1 : bin2;
             const uint64_t kpb = split && round == 0 ? (uint64_t)NT * kpt1 : kpt2 ? 2ull * NT : NT;
-            if (round == 1 && compact) {  // the survivors of round one
-                NB_HIP(hipMemsetAsync(nlive, 0, 4, st));
+            if (round == 1 && compact) {  // the survivors of round one (*nlive zeroed by
+                                          // round one's tile kernel)
                 const uint64_t per = (uint64_t)kCompactThreads * kCompactPer;
-                hipLaunchKernelGGL(probe_compact_kernel, dim3((uint32_t)((cn + per - 1) / per)),
+                const uint64_t cgrid = std::min<uint64_t>((cn + per - 1) / per, loop ? device_cus() : ~0ull);
+                hipLaunchKernelGGL(probe_compact_kernel, dim3((uint32_t)cgrid),
                                    dim3(kCompactThreads), kCompactLds, st, out + done, (uint32_t)cn, ids, nlive,
                                    gate);
                 NB_HIP(hipGetLastError());
             }
-            // (a multiple of the shards: the kernel's block classes, blockIdx % G, are equal)
-            const uint64_t bgrid = (std::min<uint64_t>((cn + kpb - 1) / kpb, bin_grid_cap) + tc.G - 1) / tc.G * tc.G;
-            hipLaunchKernelGGL(b, dim3((uint32_t)bgrid), dim3(NT),
-                               !split ? bin_lds : round == 0 ? lds1 : lds2, st, ck, co,
-                               key_len, cn, c, tc, sc, bk, words, out + done, gate, ids, nlive);
+            // (a capped grid is a multiple of kVbClasses: its counter classes are equal)
+            const uint64_t bgrid = std::min<uint64_t>((cn + kpb - 1) / kpb, bin_grid_cap);
+            const size_t blds = !split ? bin_lds : round == 0 ? lds1 : lds2;
+            if (looping) {
+                ProbeBinArgs pa{ck, co, cn, out + done, bk, words, ids, nlive, key_len, 0, c, tc, sc, gate};
+                hipLaunchKernelGGL((!split ? lbin : round == 0 ? lbin1 : lbin2), dim3((uint32_t)bgrid), dim3(NT),
+                                   blds, st, pa);
+            } else {
+                hipLaunchKernelGGL(b, dim3((uint32_t)bgrid), dim3(NT), blds, st, ck, co, key_len, cn, c, tc, sc, bk,
+                                   words, out + done, gate, ids, nlive);
+            }
             NB_HIP(hipGetLastError());
             if (!e32)
                 hipLaunchKernelGGL(tile, dim3(tc.T), dim3(kTileThreads), tile_lds, st, tc, sc,
-                                   (const uint64_t *)bk, words, nwords, out + done, gate);
+                                   (const uint64_t *)bk, words, nwords, out + done, gate, (uint32_t)cn);
             else
                 hipLaunchKernelGGL(round == 1 ? tile32i : tile32, dim3(tc.T), dim3(kTileThreads), tile_lds, st,
                                    tc, sc, (const uint32_t *)bk, words, nwords, out + done, gate, (uint32_t)kpb,
-                                   (const uint32_t *)ids);
+                                   (const uint32_t *)ids, (uint32_t)cn);
             NB_HIP(hipGetLastError());
         }
     }

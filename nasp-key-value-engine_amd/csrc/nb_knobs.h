@@ -65,8 +65,8 @@ enum Knob : int {
                         //                   block; 64 = key << 32 | offset (rounds 3-5);
                         //                   0 (default): 32 for the one-round tiled path,
                         //                   64 for the split path
-    kKnobProbeBinGrid,  // NB_PROBE_BIN_GRID tiled-probe bin kernels: blocks per CU of their
-                        //                   grid-stride grid (0: the policy, 8)
+    kKnobProbeBinGrid,  // NB_PROBE_BIN_GRID auto's gated tiled-probe bin kernels: blocks per
+                        //                   CU of their looping grid (0: the policy, 2)
     kKnobProbeHostPick, // NB_PROBE_HOST_PICK auto outside stream capture: 0 (default) the
                         //                   sample's count stays on the device and every
                         //                   path is launched gated (no host wait); 1: the

@@ -63,12 +63,13 @@ def test_build_replayed_from_graph(dev, oracle, var):
         np.testing.assert_array_equal(words.cpu().numpy().view(np.uint64), want)
 
 
-@pytest.mark.parametrize("present", [True, False])
-def test_auto_probe_replayed_from_graph(dev, oracle, present):
-    """The auto probe under stream capture: no host read-back of its sample is
-    possible, so both paths are captured and gated on the sample on the device;
-    replays on present keys (tiled chosen) and on absent keys (lane chosen) give the
-    oracle's answers."""
+def test_auto_probe_replayed_from_graph(dev, oracle):
+    """The auto probe under stream capture: its sample's count stays on the device,
+    every path (lane, tiled, split) is captured and gated on it.  One captured graph
+    replayed on present keys (tiled chosen), absent keys (lane), 30 % present (split:
+    its compaction's count and the second round's list come from the replay) and 80 %
+    present (tiled) gives the oracle's answers every time (the split
+    sequence was never the open path on a replay)."""
     import torch
     import nasp_bloom as nbm
     from nasp_bloom import synth
@@ -76,26 +77,70 @@ def test_auto_probe_replayed_from_graph(dev, oracle, present):
     base = synth.fixed_keys(n, 16, seed=71)
     words_np = oracle.build(0, base, None, 16, n, m, k, SEED)
     other = synth.fixed_keys(n, 16, seed=72)
+
+    def mixed(pc):  # keys i with i % 10 < pc / 10 present
+        b = other.copy()
+        bv, pv = b[:n * 16].reshape(n // 10, 10, 16), base[:n * 16].reshape(n // 10, 10, 16)
+        bv[:, :pc // 10] = pv[:, :pc // 10]
+        return b
     kt = torch.from_numpy(base).to(dev)
     words = torch.from_numpy(words_np.view(np.int64)).to(dev)
     out = torch.zeros(n, dtype=torch.uint8, device=dev)
     st = torch.cuda.Stream(device=dev)
-    with nbm.knobs(NB_PROBE_PATH="auto"):
-        with torch.cuda.stream(st):  # warm-up: sizes the workspace for both paths
+    with nbm.knobs(NB_PROBE_PATH="auto", NB_PROBE_SPLIT_PCT=0, NB_PROBE_TILED_PCT=0):
+        with torch.cuda.stream(st):  # warm-up: sizes the workspace for every path
             nbm.probe_device(kt, None, 16, n, m, k, SEED, 0, words, out, stream=st)
         st.synchronize()
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=st):
             nbm.probe_device(kt, None, 16, n, m, k, SEED, 0, words, out, stream=st)
-        keys = base if present else other
-        kt.copy_(torch.from_numpy(keys))
-        out.zero_()
-        torch.cuda.synchronize()
-        g.replay()
-        torch.cuda.synchronize()
-    got = out.cpu().numpy()
-    np.testing.assert_array_equal(got, oracle.probe(0, keys, None, 16, n, m, k, SEED, words_np))
-    assert got.all() == present
+        for name, keys in (("present", base), ("absent", other), ("p30", mixed(30)), ("p80", mixed(80)),
+                           ("p30 again", mixed(30))):
+            kt.copy_(torch.from_numpy(keys))
+            out.fill_(7)
+            torch.cuda.synchronize()
+            g.replay()
+            torch.cuda.synchronize()
+            got = out.cpu().numpy()
+            np.testing.assert_array_equal(got, oracle.probe(0, keys, None, 16, n, m, k, SEED, words_np),
+                                          err_msg=name)
+
+
+def test_auto_probe_does_not_wait_on_the_host(dev):
+    """nb_probe_device's contract (include/nasp_bloom.h): no host synchronisation once
+    the workspace is sized -- auto's choice is made on the device.
+    Behind ~tens of ms of queued matmuls the auto call returns at once; with
+    NB_PROBE_HOST_PICK=1 (rounds 3-5's host read-back) it waits for the queue."""
+    import time
+    import torch
+    import nasp_bloom as nbm
+    from nasp_bloom import synth
+    n, m, k = 4_200_000, 40_250_003, 7
+    kt = torch.from_numpy(synth.fixed_keys(n, 16, seed=73)).to(dev)
+    words = torch.zeros(nbm.nwords(m), dtype=torch.int64, device=dev)
+    nbm.build_device(kt, None, 16, n, m, k, SEED, 0, words)
+    out = torch.zeros(n, dtype=torch.uint8, device=dev)
+    a = torch.rand(4096, 4096, device=dev)
+    secs = {}
+    for hp in (0, 1):
+        with nbm.knobs(NB_PROBE_PATH="auto", NB_PROBE_HOST_PICK=hp):
+            nbm.probe_device(kt, None, 16, n, m, k, SEED, 0, words, out)  # sized, warm
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            b = a
+            for _ in range(40):
+                b = b @ a * 1e-3
+            t1 = time.perf_counter()
+            nbm.probe_device(kt, None, 16, n, m, k, SEED, 0, words, out)
+            t2 = time.perf_counter()
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            secs[hp] = (t2 - t1, t3 - t0)
+            assert int(out.min()) == 1
+    call0, total0 = secs[0]
+    call1, total1 = secs[1]
+    assert call0 < 0.25 * total0, secs  # enqueued behind the matmuls, not waited for
+    assert call1 > 0.5 * total1, secs   # the host pick waits for the queue and its sample
 
 
 def test_two_level_pipelined_build_replayed_from_graph(dev, oracle, knobs):

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 6: E32 bin write-out at four slots per lane -- tests, per-kernel traces.
+set -u
+export TMPDIR=/tmp
+O=gpurun_out/r06q
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_probe.py tests/test_gpu_graph.py tests/test_gpu_buckets.py > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 11; }
+tail -2 $O/tests.txt
+for b in present p30; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$b -o run --output-format csv -- python3 tools/probe_kernel_ab.py --batch $b --path tiled --entries 32 --kpts 1,2 > $O/ab_$b.txt 2>&1 || { tail -20 $O/ab_$b.txt; exit 13; }
+  echo "== $b"; grep "ms per call" $O/ab_$b.txt
+  python3 tools/trace_rounds.py $O/prof_$b/run_kernel_trace.csv | head -5
+done

@@ -136,7 +136,8 @@ def main():
     bad = 0
     for rep in range(reps):
         for label, path, chunk, pct, extra in variants:
-            with nbm.knobs(NB_PROBE_PATH=path, NB_PROBE_CHUNK=str(chunk), NB_PROBE_TILED_PCT=pct, **extra):
+            with nbm.knobs(**{"NB_PROBE_PATH": path, "NB_PROBE_CHUNK": str(chunk), "NB_PROBE_TILED_PCT": pct,
+                              **extra}):
                 for name, b in batches.items():
                     nbm.probe_device(b, offs, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out, stream=st)
                     torch.cuda.synchronize(dev)
