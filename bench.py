@@ -236,9 +236,10 @@ def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=
     # kernels at the current kernel source (tools/profile_probe.sh), C4 only
     B = (int(offs[-1].item()) + 8 * (wl.n + 1) if offs is not None else wl.n * key_len) + (wl.m + 7) // 8 + wl.n
     ppmc = latest_profile("c4_probe", "pmc") if wl.name == "c4_100M_x16B_k7_per_gpu" else None
-    for path in ("auto", "lane", "tiled", "split"):
+    for path, extra in (("auto", {}), ("lane", {}), ("tiled", {}), ("split", {}),
+                        ("auto_host_pick", {"NB_PROBE_HOST_PICK": 1})):
         r = {}
-        with nbm.knobs(NB_PROBE_PATH=path):
+        with nbm.knobs(NB_PROBE_PATH=path.split("_")[0], **extra):
             for name, kk, oo in batches:
                 with torch.cuda.stream(stream):
                     nbm.probe_device(kk, oo, key_len, wl.n, wl.m, wl.k, seed, flavor, words, out_t,
@@ -265,7 +266,9 @@ def probe_rates(wl, keys, offs, key_len, seed, flavor, words, stream, dev, reps=
         res[path] = r
     res["note"] = ("auto = the default (lane kernel on a 4 096-key sample, whose hit count picks lane, "
                    "split or tiled for the rest on the device: every path launched, the closed ones "
-                   "return at once); absent keys from another seed; p30 = keys 0-2 of every 10 "
+                   "return at once; no host wait); auto_host_pick = the same choice read back on the "
+                   "host, which then launches only the chosen path (NB_PROBE_HOST_PICK=1, rounds 3-5: "
+                   "blocks the caller on the sample); absent keys from another seed; p30 = keys 0-2 of every 10 "
                    "present, the rest absent; ms = wall clock per call over 5 back-to-back calls "
                    "between device synchronisations; roofline: algorithmic bytes (keys + filter + "
                    "answers) / ms, traffic and device_us from the committed probe PMC summary ("
