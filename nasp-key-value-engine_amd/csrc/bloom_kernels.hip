@@ -1587,11 +1587,11 @@ __host__ __device__ constexpr uint32_t probe_sort_offset_words(uint32_t T) {
 // per run, the run's header slot (by the thread reserving it) and every index placed
 // behind it as its 32-bit entry.  In LDS a header slot holds 0x80000000 | t: the
 // write-out (each wave one contiguous range of slots, 64 at a time) finds a slot's
-// tile with the same "last header" wave scan the tile kernel uses, so the sort area
-// is 4 B per slot -- two blocks of 2 048 keys fit a CU -- and stores the bin block's
-// header word 0x80000000 | vb in its place.  An entry past its bucket's capacity
+// tile as a wave-wide running maximum (the tiles ascend along the slots), so the sort
+// area is 4 B per slot -- two blocks of 2 048 keys fit a CU -- and stores the bin
+// block's header word 0x80000000 | vb in its place.  An entry past its bucket's capacity
 // (duplicated keys only) is tested right here.
-__device__ __forceinline__ uint32_t wave_last_nonzero(uint32_t v);
+__device__ __forceinline__ uint32_t wave_inclusive_max(uint32_t v);
 template <int NT, int PKPT, int KR, int J0, int J1, bool IDS, class PH>
 __device__ __forceinline__ void probe_bin_tail_e32(uint32_t vb, const PH &ph, const TileCfg &tc, const TileScratch &sc,
                                                    uint32_t *cnt, uint32_t *S, uint32_t *GX, uint32_t *L,
@@ -1605,12 +1605,14 @@ __device__ __forceinline__ void probe_bin_tail_e32(uint32_t vb, const PH &ph, co
     const uint32_t total = block_exclusive_scan<NT>(cnt, S, T, wave_sums);
     const uint32_t shard = vb & (tc.G - 1);
     uint32_t *cur = sc.gcur + (size_t)shard * T;
+    uint2 *GXL = reinterpret_cast<uint2 *>(GX);  // [T] {run table, capacity limit} (GX | L, 2T words)
     for (uint32_t t = tid; t < T; t += NT) {
         const uint32_t h = cnt[t], g = h ? atomicAdd(&cur[t], h) : 0u;
-        GX[t] = bucket_region(tc, t, shard) * tc.cap + g - S[t];
-        L[t] = S[t] + (g < tc.cap ? tc.cap - g : 0u);
+        GXL[t] = make_uint2(bucket_region(tc, t, shard) * tc.cap + g - S[t],
+                            S[t] + (g < tc.cap ? tc.cap - g : 0u));
         if (h) sword[S[t]] = 0x80000000u | t;
     }
+    (void)L;
     // placement behind the header slot (the reservations' round trips overlap it)
     const uint32_t msk = (1u << tc.ts) - 1, b32 = (uint32_t)base;
 #pragma unroll
@@ -1630,33 +1632,39 @@ __device__ __forceinline__ void probe_bin_tail_e32(uint32_t vb, const PH &ph, co
     // write-out: each wave one contiguous range of slots, 64 at a time (one slot per
     // lane: a store instruction covers ~7 runs.  Four slots per lane -- one 16-byte LDS
     // read and one tile scan per 256 slots -- measured slower, 0.87 -> 1.02 ms per 50M
-    // keys: each store instruction then spans ~28 runs, profiles/r06r_probe_trace.txt)
+    // keys: each store instruction then spans ~28 runs, profiles/r06r_probe_trace.txt).
+    // The tiles ascend along the slots and a header slot holds 0x80000000 | t, above
+    // every entry word, so the header in force at a slot is the running maximum of the
+    // raw words: one DPP max per step (a select-based "last header" scan cost 4 VALU a
+    // step, and the loop ~45 VALU per 64 slots).
     constexpr uint32_t kW = NT / 64;
     const uint32_t per = (total + kW - 1) / kW;
     const uint32_t s0 = min(wid * per, total), s1 = min(s0 + per, total);
     if (s0 >= s1) return;  // wave-uniform; no barrier follows
-    // the tile in force at s0 (+1; slot 0 is a header)
-    uint32_t carry = 0;
-    for (uint32_t b = s0; b > 0 && carry == 0; b = b > 64 ? b - 64 : 0) {
+    // the header in force at s0 (slot 0 is a header)
+    uint32_t carry = 0x80000000u;
+    for (uint32_t b = s0; b > 0; b = b > 64 ? b - 64 : 0) {
         const bool in = lane < b;
         const uint32_t w = in ? sword[b - 1 - lane] : 0u;
         const uint64_t hm = __ballot(in && (w >> 31));
-        if (hm) carry = (__shfl(w, (int)__builtin_ctzll(hm)) & 0x7fffffffu) + 1;
+        if (hm) {
+            carry = __shfl(w, (int)__builtin_ctzll(hm));
+            break;
+        }
     }
     const uint32_t hdr = 0x80000000u | vb;
     for (uint32_t q0 = s0; q0 < s1; q0 += 64) {
         const uint32_t q = q0 + lane;
         const bool valid = q < s1;
         const uint32_t w = valid ? sword[q] : 0u;
-        const bool is_hdr = valid && (w >> 31);
-        const uint32_t X = wave_last_nonzero(is_hdr ? (w & 0x7fffffffu) + 1 : 0u);
-        const uint32_t t = (X ? X : carry) - 1;
-        const uint32_t tail = __builtin_amdgcn_readlane(X, 63);
-        if (tail) carry = tail;
-        if (!valid) continue;
-        if (q < L[t]) {
-            buckets[(uint32_t)(GX[t] + q)] = is_hdr ? hdr : w;
-        } else if (!is_hdr) {
+        const uint32_t X = max(wave_inclusive_max(w), carry);
+        carry = __builtin_amdgcn_readlane(X, 63);
+        const uint32_t t = X & 0x7fffffffu;
+        const uint2 gl = GXL[t];
+        const bool is_hdr = w >> 31;
+        if (valid && q < gl.y) {
+            buckets[(uint32_t)(gl.x + q)] = is_hdr ? hdr : w;
+        } else if (valid && !is_hdr) {
             const uint32_t v = (t << tc.ts) | (w & msk);
             if (!((words[v >> 6] >> (v & 63)) & 1u)) {
                 const uint32_t j = b32 + (w >> tc.ts);
@@ -1664,6 +1672,18 @@ __device__ __forceinline__ void probe_bin_tail_e32(uint32_t vb, const PH &ph, co
             }
         }
     }
+}
+
+// Inclusive maximum across a wave64 (the wave_inclusive_scan pattern with max for add;
+// 0 is max's identity, so lanes whose DPP source is out of range are unaffected).
+__device__ __forceinline__ uint32_t wave_inclusive_max(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, false));  // row_shr:1
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, false));  // row_shr:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, false));  // row_shr:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, false));  // row_shr:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return v;
 }
 
 // Inclusive "last nonzero" scan across a wave64 (the wave_inclusive_scan pattern with
