@@ -39,8 +39,9 @@ def main():
                          "from --fill-keys device-random keys (the present keys among them); c3: "
                          "C3's 100M variable-length keys (8-64 B) and filter, the absent keys "
                          "the same keys with their first byte changed (same offsets)")
-    ap.add_argument("--entries", default="32",
-                    help="tiled / split variants at these NB_PROBE_ENTRY formats (32,64: an A/B)")
+    ap.add_argument("--entries", default="0",
+                    help="tiled / split variants at these NB_PROBE_ENTRY formats (0: the policy -- "
+                         "32-bit one-round, 64-bit split; 32,64: an A/B forcing either)")
     ap.add_argument("--variant", action="append", default=[],
                     help="extra variant LABEL:PATH:KNOB=V,KNOB=V (repeatable), e.g. "
                          "'auto-host:auto:NB_PROBE_HOST_PICK=1'")
