@@ -82,11 +82,12 @@ uint64_t nb_device_merkle_count(void);
  * 3 split: the tiled probe in two rounds), NB_PROBE_SPLIT_PCT (auto, k > 2: the split
  * path from this percentage of present keys in its sample up to 65 for 16- / 32-byte
  * keys at k <= 8, 55 above, 40 for variable-length keys; default 0, the policy: 7 for
- * 16- / 32-byte keys at k <= 8, 18 otherwise; > 100: never),
+ * 16- / 32-byte keys at k <= 8, 18 otherwise, on batches of 2^24 keys or more at k > 3,
+ * never on smaller batches or at k = 3; > 100: never),
  * NB_PROBE_CHUNK (keys per tiled-probe pass; 0: the policy), NB_PROBE_TILED_PCT (auto's
  * tiled path from this percentage of present keys in its sample; default 0, the policy:
- * the split policy's upper bound above, 30 when auto never splits; a split threshold at
- * or above it leaves the two-way choice), NB_PROBE_ENTRY (tiled-probe bucket entries:
+ * the split policy's upper bound above, 10 where the policy leaves the split path out,
+ * 30 at k <= 2; a split threshold at or above it leaves the two-way choice), NB_PROBE_ENTRY (tiled-probe bucket entries:
  * 32 or 64 bits everywhere; default 0: 32 for the one-round tiled path, 64 for the
  * split path), NB_PROBE_BIN_GRID (blocks per CU of auto's gated, looping tiled-probe bin
  * kernels; 0: 2), NB_PROBE_KPT (keys per bin thread of the one-round 32-bit path; 0:
@@ -237,7 +238,10 @@ int nb_build_device_ex(const uint8_t *d_keys, const uint64_t *d_offsets, uint32_
  * key and picks from the share of them present: the lane path below NB_PROBE_SPLIT_PCT
  * (the policy: 7 % for 16- / 32-byte keys at k <= 8, 18 % otherwise), the split path
  * up to 65 % (55 % for k > 8, 40 % for variable-length keys), the tiled path from
- * there (NB_PROBE_SPLIT_PCT > 100: the tiled path from 30 %).  The choice is made on
+ * there.  The policy leaves the split path out below 2^24 keys and at k = 3 (the lane
+ * path below 10 %, the tiled path from there; NB_PROBE_SPLIT_PCT > 100: the same
+ * two-way choice everywhere), and a filter of at most 2^25 bits (4 MiB: one XCD's L2 holds it) takes the
+ * lane path without a sample.  The choice is made on
  * the device: every path is launched behind the sample and gated on its count, so
  * auto never waits on the host (NB_PROBE_HOST_PICK=1 restores rounds 3-5's host
  * read-back outside graph capture).  The one-round tiled path's bucket entries are

@@ -2881,6 +2881,15 @@ size_t probe_bin_lds_bytes(uint32_t T, uint32_t keff, bool stage, bool e32 = fal
 constexpr uint32_t kProbeSampleBlocks = 16;                 // one key per lane
 constexpr uint64_t kProbeSample = kProbeSampleBlocks * kBlock;  // 4 096 keys
 constexpr uint64_t kProbeTiledMin = 1 << 22;
+// Auto's choice settled by shape (round 6, measured on shapes the sample thresholds
+// were not fitted to, profiles/r06sh_auto_shapes.txt): a filter of at most
+// kProbeL2Bits bits fits each XCD's 4 MB L2, and the lane kernel's gathers hit there;
+// below kProbeSplitMin keys, or at k = 3 (the first round's two indices leave one),
+// the split path stays out -- its five gated launches cost more than it saves -- and
+// lane / tiled split at kProbeTwoWayPct present.
+constexpr uint64_t kProbeL2Bits = 1ull << 25;
+constexpr uint64_t kProbeSplitMin = 1 << 24;
+constexpr uint32_t kProbeTwoWayPct = 10;
 
 template <int FLAVOR, int LAYOUT>
 int launch_probe_lane(const uint8_t *keys, const uint64_t *offsets, uint32_t key_len, uint64_t n,
@@ -3075,21 +3084,25 @@ int launch_probe_l(const uint8_t *keys, const uint64_t *offsets, uint32_t key_le
                           probe_bin_lds_bytes(pT, c.k, !vec_layout(LAYOUT), false) <= kMaxBlockLds &&
                           probe_bin_lds_bytes(pT, c.k, !vec_layout(LAYOUT), true) <= kMaxBlockLds;
     const ProbeGate none{nullptr, nullptr, 0, 0, 0};
-    // the split path takes part in auto's choice wherever the tiled path does (k > 2).
-    // NB_PROBE_TILED_PCT set (non-zero) is honoured as the threshold of the tiled path;
-    // at 0 it is the policy: split_tiled_pct when the split path takes part, else 30.
-    // A split threshold at or above the tiled one leaves the two-way choice.
+    // the split path takes part in auto's choice where the tiled path does (k > 2), on
+    // batches of kProbeSplitMin keys or more and k > 3 -- or wherever NB_PROBE_SPLIT_PCT
+    // is set.  NB_PROBE_TILED_PCT set (non-zero) is honoured as the threshold of the
+    // tiled path; at 0 it is the policy: split_tiled_pct when the split path takes part,
+    // kProbeTwoWayPct where it is left out (by the policy or NB_PROBE_SPLIT_PCT > 100),
+    // 30 at k <= 2 (not measured since round 4).  A split threshold at or above the tiled one leaves the two-way choice
+    // (ADVICE r05).
     constexpr bool kVec = vec_layout(LAYOUT);
     const uint64_t tpk = knob(nb::kKnobProbeTiledPct), spk = knob(nb::kKnobProbeSplitPct);
-    uint32_t pct = tpk ? (uint32_t)std::min<uint64_t>(tpk, 101) : 30u;
-    uint32_t split_pct = c.k <= (uint32_t)kSplitJ ? 101u
+    const bool split_out = c.k <= (uint32_t)kSplitJ || (!spk && (c.k <= 3 || n < kProbeSplitMin));
+    uint32_t pct = tpk ? (uint32_t)std::min<uint64_t>(tpk, 101) : c.k <= (uint32_t)kSplitJ ? 30u : kProbeTwoWayPct;
+    uint32_t split_pct = split_out ? 101u
                          : spk ? (uint32_t)std::min<uint64_t>(spk, 101) : split_pct_policy(c.k, kVec);
     if (split_pct <= 100) {
         const uint32_t to_tiled = tpk ? pct : split_tiled_pct(c.k, kVec);
         if (split_pct < to_tiled) pct = to_tiled;
         else split_pct = 101;
     }
-    if (path == 1 || !tiled_ok || (path == 0 && n < kProbeTiledMin))
+    if (path == 1 || !tiled_ok || (path == 0 && (n < kProbeTiledMin || c.fm.m <= kProbeL2Bits)))
         return launch_probe_lane<FLAVOR, LAYOUT>(keys, offsets, key_len, n, c, words, out, st, none);
     auto tiled = [&](const uint8_t *k_, const uint64_t *o_, uint64_t n_, uint8_t *out_,
                      const ProbeGate &g, bool split = false) -> int {

@@ -69,7 +69,8 @@ def test_auto_probe_replayed_from_graph(dev, oracle):
     replayed on present keys (tiled chosen), absent keys (lane), 30 % present (split:
     its compaction's count and the second round's list come from the replay) and 80 %
     present (tiled) gives the oracle's answers every time (the split
-    sequence was never the open path on a replay)."""
+    sequence was never the open path on a replay).  NB_PROBE_SPLIT_PCT=7 keeps the split
+    path in the choice at this size (the policy leaves it out below 2^24 keys)."""
     import torch
     import nasp_bloom as nbm
     from nasp_bloom import synth
@@ -87,7 +88,7 @@ def test_auto_probe_replayed_from_graph(dev, oracle):
     words = torch.from_numpy(words_np.view(np.int64)).to(dev)
     out = torch.zeros(n, dtype=torch.uint8, device=dev)
     st = torch.cuda.Stream(device=dev)
-    with nbm.knobs(NB_PROBE_PATH="auto", NB_PROBE_SPLIT_PCT=0, NB_PROBE_TILED_PCT=0):
+    with nbm.knobs(NB_PROBE_PATH="auto", NB_PROBE_SPLIT_PCT=7, NB_PROBE_TILED_PCT=0):
         with torch.cuda.stream(st):  # warm-up: sizes the workspace for every path
             nbm.probe_device(kt, None, 16, n, m, k, SEED, 0, words, out, stream=st)
         st.synchronize()

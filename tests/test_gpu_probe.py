@@ -146,6 +146,27 @@ def test_tiled_probe_c4_full_size(dev, knobs):
     assert 0.008 < fp < 0.012
 
 
+@pytest.mark.parametrize("m, k, n", [(2**25, 4, 4_500_000), (2**25 + 1, 4, 4_500_000),
+                                     (40_250_003, 3, 16_800_000), (95_850_584, 5, 16_800_000)])
+@pytest.mark.parametrize("pc", [0, 30, 100])
+def test_auto_policy_boundaries(dev, oracle, knobs, m, k, n, pc):
+    """Auto at the shape rules' edges (round 6, profiles/r06sh_auto_shapes.txt): a
+    filter of 2^25 bits (lane, no sample) and one bit more (lane / tiled at 10 %);
+    k = 3 (no split round) and k = 5 at 2^24 + 22 784 keys (split back in the choice),
+    each on absent, 30 % present and present batches, bit-exact against the oracle."""
+    from nasp_bloom import synth
+    knobs(NB_PROBE_PATH="auto", NB_PROBE_SPLIT_PCT="0", NB_PROBE_TILED_PCT="0")
+    base = synth.fixed_keys(n, 16, seed=31)
+    words = oracle.build(0, base, None, 16, n // 2, m, k, SEED)
+    batch = synth.fixed_keys(n, 16, seed=32)
+    idx = np.nonzero(np.arange(n) % 10 < pc // 10)[0]
+    bv, pv = batch[: n * 16].reshape(n, 16), base[: n * 16].reshape(n, 16)
+    bv[idx] = pv[idx % (n // 2)]
+    got = dev_probe(dev, batch, None, 16, n, m, k, SEED, words)
+    np.testing.assert_array_equal(got, oracle.probe(0, batch, None, 16, n, m, k, SEED, words))
+    assert got[idx].all()
+
+
 @pytest.mark.parametrize("path", ["tiled", "split", "auto"])
 @pytest.mark.parametrize("k", [11, 12, 16])
 def test_probe_32byte_keys_large_k_full_filter(dev, oracle, knobs, path, k):
@@ -167,13 +188,14 @@ def test_probe_32byte_keys_large_k_full_filter(dev, oracle, knobs, path, k):
 
 
 @pytest.mark.parametrize("shape", ["c4_fixed16", "c5_fixed32_k10"])
-@pytest.mark.parametrize("split_pct", ["0", "101"])
+@pytest.mark.parametrize("split_pct", ["0", "7", "101"])
 @pytest.mark.parametrize("pc", [5, 30, 70])
 def test_auto_mixed_batches(dev, oracle, knobs, probe_shapes, pc, split_pct, shape):
     """Auto on batches whose sample sees pc % present keys (every key i with
-    i % 20 < pc / 5 present): lane, split (NB_PROBE_SPLIT_PCT 0, the policy: from 7 %
-    at k <= 8, 18 % above, to 65 % / 55 %) or tiled, bit-exact against the oracle whichever it
-    picks; NB_PROBE_SPLIT_PCT=101 leaves the two-way choice."""
+    i % 20 < pc / 5 present): lane, split (NB_PROBE_SPLIT_PCT=7: from 7 % to 65 % / 55 %)
+    or tiled, bit-exact against the oracle whichever it picks; NB_PROBE_SPLIT_PCT 0 is
+    the policy, which at 4.5M keys (< 2^24) leaves the split path out (lane / tiled at
+    10 %), as does NB_PROBE_SPLIT_PCT=101."""
     from nasp_bloom import synth
     buf, offs, kl, n, m, k, fl = probe_shapes[shape]
     knobs(NB_PROBE_PATH="auto", NB_PROBE_SPLIT_PCT=split_pct)
@@ -194,10 +216,11 @@ def test_auto_mixed_batches(dev, oracle, knobs, probe_shapes, pc, split_pct, sha
 def test_auto_mixed_batches_varlen(dev, oracle, knobs, probe_shapes, pc):
     """The same for variable-length keys (C3's shape): the filter of all the keys, the
     batch the same keys with the first byte changed except where i % 20 < pc / 5 --
-    lane, split (18-40 %: its second round hashes the listed keys straight from HBM) or
-    tiled, bit-exact against the oracle."""
+    lane, split (NB_PROBE_SPLIT_PCT=18, the policy's threshold on larger batches: 18-40 %;
+    its second round hashes the listed keys straight from HBM) or tiled, bit-exact
+    against the oracle."""
     buf, offs, kl, n, m, k, fl = probe_shapes["c3_varlen"]
-    knobs(NB_PROBE_PATH="auto", NB_PROBE_SPLIT_PCT="0")
+    knobs(NB_PROBE_PATH="auto", NB_PROBE_SPLIT_PCT="18")
     words = device_words(dev, buf, offs, kl, n, m, k, fl)
     keep = np.arange(n) % 20 < pc // 5
     mixed = buf.copy()

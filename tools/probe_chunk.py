@@ -33,12 +33,13 @@ def main():
     ap.add_argument("--no-lane", action="store_true")
     ap.add_argument("--split", action="store_true", help="also the split tiled probe (two rounds)")
     ap.add_argument("--auto-pct", default="", help="auto path at these NB_PROBE_TILED_PCT values ('policy' = 0)")
-    ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c3"],
+    ap.add_argument("--workload", default="c4", choices=["c4", "c5", "c3", "shape"],
                     help="c4: C4's filter from the 100M probed present keys; c5: C5's shape "
                          "(m = 2^32-1, k = 10, 32-byte keys), --n probed keys, the filter built "
                          "from --fill-keys device-random keys (the present keys among them); c3: "
                          "C3's 100M variable-length keys (8-64 B) and filter, the absent keys "
-                         "the same keys with their first byte changed (same offsets)")
+                         "the same keys with their first byte changed (same offsets); shape: "
+                         "as c5 at --m / --k / --key-len, the filter half full unless --fill-keys")
     ap.add_argument("--entries", default="0",
                     help="tiled / split variants at these NB_PROBE_ENTRY formats (0: the policy -- "
                          "32-bit one-round, 64-bit split; 32,64: an A/B forcing either)")
@@ -46,8 +47,13 @@ def main():
                     help="extra variant LABEL:PATH:KNOB=V,KNOB=V (repeatable), e.g. "
                          "'auto-host:auto:NB_PROBE_HOST_PICK=1'")
     ap.add_argument("--n", type=int, default=50_000_000)
-    ap.add_argument("--fill-keys", type=int, default=400_000_000)
+    ap.add_argument("--fill-keys", type=int, default=0, help="c5 / shape (0: 400M for c5, m ln2 / k for shape)")
+    ap.add_argument("--m", type=int, default=0)
+    ap.add_argument("--k", type=int, default=0)
+    ap.add_argument("--key-len", type=int, default=0)
     args = ap.parse_args()
+    if args.workload == "shape" and not (args.m and args.k and args.key_len):
+        ap.error("--workload shape needs --m, --k and --key-len")
     reps = args.reps
     dev = torch.device("cuda", 0)
     st = torch.cuda.Stream(device=dev)
@@ -75,12 +81,23 @@ def main():
         present = torch.from_numpy(p_np).to(dev)
         absent = torch.from_numpy(a_np).to(dev)
     else:
-        wl = synth.Workload("c5_shape_probe", args.n, 32, synth.C5.m, synth.C5.k, 0.01)
-        kl = 32
+        if args.workload == "c5":
+            wl = synth.Workload("c5_shape_probe", args.n, 32, synth.C5.m, synth.C5.k, 0.01)
+            args.fill_keys = args.fill_keys or 400_000_000
+        else:  # (p is a label only: the probe takes m and k)
+            wl = synth.Workload(f"shape_m{args.m}_k{args.k}_L{args.key_len}", args.n, args.key_len,
+                                args.m, args.k, 0.01)
+            args.fill_keys = args.fill_keys or int(args.m * np.log(2) / args.k)
+        kl = wl.key_len
         g = torch.Generator(device=dev)
         g.manual_seed(5)
         fill = torch.randint(0, 256, (args.fill_keys * kl + 64,), dtype=torch.uint8, device=dev, generator=g)
-        present = fill[:wl.n * kl + 64].clone()
+        if args.fill_keys >= wl.n:
+            present = fill[:wl.n * kl + 64].clone()
+        else:  # (a filter smaller than the batch: the filled keys, repeated)
+            rep = -(-wl.n // args.fill_keys)
+            present = torch.cat([fill[:args.fill_keys * kl].repeat(rep)[:wl.n * kl],
+                                 torch.zeros(64, dtype=torch.uint8, device=dev)])
         absent = torch.randint(0, 256, (wl.n * kl + 64,), dtype=torch.uint8, device=dev, generator=g)
     want_b = args.batches.split(",")
     if offs is not None:
@@ -102,6 +119,7 @@ def main():
         batches[f"p{pc}"] = b
     batches = {b: batches[b] for b in args.batches.split(",")}
     words = torch.zeros(nbm.nwords(wl.m), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize(dev)  # (the keys and the zeroed words, made on the current stream, before st uses them)
     if fill is None:
         nbm.build_device(present, offs, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, stream=st,
                          overwrite=True)
@@ -120,6 +138,7 @@ def main():
             nbm.probe_device(b, offs, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out, stream=st)
             torch.cuda.synchronize(dev)
             ref[name] = out.clone()
+            torch.cuda.synchronize(dev)  # (the copy, on the current stream, before st writes out again)
     ents = [int(e) for e in args.entries.split(",")]
 
     def ent(e):
@@ -144,7 +163,10 @@ def main():
                     torch.cuda.synchronize(dev)
                     if not torch.equal(out, ref[name]):
                         bad += 1
-                        print(f"MISMATCH {label} {name}", flush=True)
+                        d = torch.nonzero(out != ref[name]).flatten()
+                        print(f"MISMATCH {label} {name}: {d.numel()} answers, first at "
+                              f"{d[:4].tolist()} (got {out[d[:4]].tolist()}, lane {ref[name][d[:4]].tolist()})",
+                              flush=True)
                     t0 = time.perf_counter()
                     for _ in range(5):
                         nbm.probe_device(b, offs, kl, wl.n, wl.m, wl.k, synth.H2_SEED, 0, words, out,
